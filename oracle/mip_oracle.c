@@ -1,0 +1,387 @@
+/* mip_oracle.c -- TEST INFRASTRUCTURE ONLY (see mip_oracle.h).
+ *
+ * A deliberately plain, scalar restatement of the reference algorithm, one CU and one
+ * mode at a time, in frame coordinates.  No tiling, no vectorisation: readability is
+ * the point; it is the checker for the HIP path, never part of it.
+ *
+ * Reference anchors (iagostorch/VVC-MIP-GPU @ /root/reference):
+ *   boundaries          intra.cl:17-344   (initBoundaries)
+ *   reduced prediction  intra.cl:349-543  (MIP_ReducedPred), weights mip_matrix.cl
+ *   upsampling          intra.cl:815-912  (upsampleDistortion, horizontal then vertical)
+ *   SAD / SATD / cost   intra.cl:922-1166, kernel_aux_functions.cl:142-249 (satd_4x4)
+ *   2-D filters         intra.cl:2856-3040, 1639-1826, 3042-3265, 2311-2537
+ *   separable filters   intra.cl:3267-3506, 1828-2087, 3508-3823, 2539-2854
+ *   cost layout         constants.h:1558-1631 (ALL_stridedDistortionsPerCtu)
+ */
+#include "mip_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../vvc-mip-gpu_amd/csrc/mip_tables.h"
+
+static const mip_shape_desc SHAPES[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;
+static const uint8_t W_S0[16 * 16 * 4] = MIP_WEIGHTS_S0;
+static const uint8_t W_S1[8 * 16 * 8] = MIP_WEIGHTS_S1;
+static const uint8_t W_S2[6 * 64 * 7] = MIP_WEIGHTS_S2;
+static const uint16_t TAPS3[5 * 9] = MIP_TAPS_3x3;
+static const uint16_t TAPS5[3 * 25] = MIP_TAPS_5x5;
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) l++;
+  return l;
+}
+
+static int axis_pos(int base, int step, int dual, int i) {
+  return dual ? base + (i / 2) * step + (i % 2) * dual : base + i * step;
+}
+
+int mipo_num_ctus(int width, int height) {
+  return ((width + 127) / 128) * ((height + 127) / 128); /* intra.cl:31-33 */
+}
+
+int64_t mipo_costs_per_frame(int width, int height) {
+  return (int64_t)mipo_num_ctus(width, height) * MIP_COSTS_PER_CTU;
+}
+
+/* ---------------------------------------------------------------- boundaries --- */
+
+/* Complete and reduced boundaries of the CU at frame position (x, y).
+ * Padding rules intra.cl:96-107 (top) and 232-243 (left); box downsampling with
+ * (sum + 2^(log2 df - 1)) >> log2 df, intra.cl:71-73, 127-141, 202-204, 259-279.
+ * A downsampling factor of 1 is a plain copy (the OpenCL `1 << -1` rounding term
+ * truncates to 0 in a short, intra.cl:73). */
+void mipo_cu_boundaries(const uint16_t *refs, int width, int height, int x, int y, int w,
+                        int h, int16_t *top, int16_t *left, int16_t *red_top,
+                        int16_t *red_left) {
+  (void)height;
+  for (int i = 0; i < w; i++) {
+    int v;
+    if (y > 0) v = refs[(size_t)(y - 1) * width + x + i];
+    else if (x == 0) v = 512;
+    else v = refs[x - 1];
+    top[i] = (int16_t)v;
+  }
+  for (int i = 0; i < h; i++) {
+    int v;
+    if (x > 0) v = refs[(size_t)(y + i) * width + x - 1];
+    else if (y == 0) v = 512;
+    else v = refs[(size_t)(y - 1) * width];
+    left[i] = (int16_t)v;
+  }
+  const int rbs = (w == 4 && h == 4) ? 2 : 4;
+  for (int side = 0; side < 2; side++) {
+    const int n = side ? h : w;
+    const int16_t *src = side ? left : top;
+    int16_t *dst = side ? red_left : red_top;
+    const int df = n / rbs, l2 = ilog2(df), rnd = df > 1 ? 1 << (l2 - 1) : 0;
+    for (int i = 0; i < rbs; i++) {
+      int s = 0;
+      for (int t = 0; t < df; t++) s += src[i * df + t];
+      dst[i] = (int16_t)((s + rnd) >> l2);
+    }
+  }
+}
+
+/* --------------------------------------------------------- reduced prediction --- */
+
+/* Matrix-vector product of one mode, intra.cl:415-487.  Output stored at the
+ * transposed position for transposed modes (intra.cl:402-406, 485). */
+void mipo_reduced_pred(int size_id, int mode, int transposed, const int16_t *red_top,
+                       const int16_t *red_left, int16_t *pred) {
+  const int rbs = size_id == 0 ? 2 : 4;
+  const int r = size_id == 2 ? 8 : 4;
+  const int nin = 2 * rbs;
+  int b[8];
+  for (int i = 0; i < rbs; i++) {
+    b[i] = transposed ? red_left[i] : red_top[i];
+    b[rbs + i] = transposed ? red_top[i] : red_left[i];
+  }
+  const int b0 = b[0];
+  int p[8];
+  for (int i = 0; i < nin; i++) p[i] = b[i] - b0;
+  p[0] = size_id == 2 ? 0 : (1 << 9) - b0; /* intra.cl:446 */
+  int psum = 0;
+  for (int i = 0; i < nin; i++) psum += p[i];
+  const int offset = 32 - 32 * psum; /* intra.cl:449-454 */
+  for (int j = 0; j < r * r; j++) {
+    int acc = offset;
+    for (int i = 0; i < nin; i++) {
+      int w;
+      if (size_id == 2) w = i == 0 ? 0 : W_S2[(mode * 64 + j) * 7 + i - 1]; /* 459-463 */
+      else if (size_id == 1) w = W_S1[(mode * 16 + j) * 8 + i];
+      else w = W_S0[(mode * 16 + j) * 4 + i];
+      acc += p[i] * w;
+    }
+    int v = (acc >> 6) + b0;
+    v = v < 0 ? 0 : (v > 1023 ? 1023 : v);
+    const int pos = transposed ? (j % r) * r + j / r : j;
+    pred[pos] = (int16_t)v;
+  }
+}
+
+/* ------------------------------------------------------------------ upsampling --- */
+
+/* intra.cl:815-912: horizontal pass on rows k*upV + upV-1 (left boundary as the
+ * "before" sample of the first window), then vertical pass on every row (top
+ * boundary as "before").  Factor 1 = copy. */
+static void upsample(const int16_t *red, int r, int w, int h, const int16_t *top,
+                     const int16_t *left, int16_t *out) {
+  const int uh = w / r, uv = h / r, lh = ilog2(uh), lv = ilog2(uv);
+  for (int k = 0; k < r; k++) {
+    const int ya = k * uv + uv - 1;
+    for (int x = 0; x < w; x++) {
+      int v;
+      if (uh == 1) {
+        v = red[k * r + x];
+      } else {
+        const int o = x % uh + 1;
+        const int before = x < uh ? left[ya] : red[k * r + (x >> lh) - 1];
+        const int after = red[k * r + (x >> lh)];
+        v = ((uh - o) * before + o * after + (1 << (lh - 1))) >> lh;
+      }
+      out[ya * w + x] = (int16_t)v;
+    }
+  }
+  if (uv == 1) return;
+  for (int y = 0; y < h; y++) {
+    if (y % uv == uv - 1) continue; /* anchor rows keep their value */
+    const int o = y % uv + 1, kk = y >> lv;
+    for (int x = 0; x < w; x++) {
+      const int before = y < uv ? top[x] : out[(kk * uv - 1) * w + x];
+      const int after = out[(kk * uv + uv - 1) * w + x];
+      out[y * w + x] = (int16_t)(((uv - o) * before + o * after + (1 << (lv - 1))) >> lv);
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ distortion --- */
+
+static int iabs(int v) { return v < 0 ? -v : v; }
+
+/* 4x4 Hadamard SATD as in kernel_aux_functions.cl:142-249 (VTM xCalcHADs4x4 with the
+ * JVET_R0164 DC scaling and final (satd+1)>>1). */
+static int satd4x4(const int *d) {
+  int m[16], e[16];
+  for (int i = 0; i < 4; i++) {
+    m[i] = d[i] + d[12 + i];
+    m[4 + i] = d[4 + i] + d[8 + i];
+    m[8 + i] = d[4 + i] - d[8 + i];
+    m[12 + i] = d[i] - d[12 + i];
+  }
+  for (int i = 0; i < 4; i++) {
+    e[i] = m[i] + m[4 + i];
+    e[4 + i] = m[8 + i] + m[12 + i];
+    e[8 + i] = m[i] - m[4 + i];
+    e[12 + i] = m[12 + i] - m[8 + i];
+  }
+  for (int row = 0; row < 4; row++) {
+    const int *s = e + 4 * row;
+    int t0 = s[0] + s[3], t1 = s[1] + s[2], t2 = s[1] - s[2], t3 = s[0] - s[3];
+    m[4 * row + 0] = t0 + t1;
+    m[4 * row + 1] = t0 - t1;
+    m[4 * row + 2] = t2 + t3;
+    m[4 * row + 3] = t3 - t2;
+  }
+  int satd = 0;
+  for (int k = 0; k < 16; k++) satd += iabs(m[k]);
+  satd -= iabs(m[0]);
+  satd += iabs(m[0]) >> 2;
+  return (satd + 1) >> 1;
+}
+
+static void cu_distortion(const uint16_t *orig, int width, int x, int y, int w, int h,
+                          const int16_t *pred, int *sad_out, int *satd_out) {
+  int sad = 0, satd = 0;
+  for (int yy = 0; yy < h; yy++)
+    for (int xx = 0; xx < w; xx++)
+      sad += iabs((int)orig[(size_t)(y + yy) * width + x + xx] - pred[yy * w + xx]);
+  for (int by = 0; by < h; by += 4)
+    for (int bx = 0; bx < w; bx += 4) {
+      int d[16];
+      for (int i = 0; i < 16; i++) {
+        const int yy = by + i / 4, xx = bx + i % 4;
+        d[i] = (int)orig[(size_t)(y + yy) * width + x + xx] - pred[yy * w + xx];
+      }
+      satd += satd4x4(d);
+    }
+  *sad_out = sad;
+  *satd_out = satd;
+}
+
+/* ---------------------------------------------------------------------- search --- */
+
+static void search_ctu(const uint16_t *orig, const uint16_t *refs, int width, int height,
+                       int ctu, int32_t *cost, int32_t *sad, int32_t *satd) {
+  const int ctu_cols = (width + 127) / 128;
+  const int cx = 128 * (ctu % ctu_cols), cy = 128 * (ctu / ctu_cols);
+  int16_t top[64], left[64], rt[4], rl[4], red[64], pred[64 * 64];
+  for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+    const mip_shape_desc *sd = &SHAPES[s];
+    const int w = sd->w, h = sd->h, nm = 2 * sd->modes, r = sd->size_id == 2 ? 8 : 4;
+    for (int cu = 0; cu < sd->ncu; cu++) {
+      const int x = cx + axis_pos(sd->xb, sd->xs, sd->xd, cu % sd->ncols);
+      const int y = cy + axis_pos(sd->yb, sd->ys, sd->yd, cu / sd->ncols);
+      const size_t base = (size_t)ctu * MIP_COSTS_PER_CTU + sd->cost_offset + (size_t)cu * nm;
+      if (x + w > width || y + h > height) {
+        for (int m = 0; m < nm; m++) {
+          cost[base + m] = MIPO_UNAVAILABLE;
+          if (sad) sad[base + m] = MIPO_UNAVAILABLE;
+          if (satd) satd[base + m] = MIPO_UNAVAILABLE;
+        }
+        continue;
+      }
+      mipo_cu_boundaries(refs, width, height, x, y, w, h, top, left, rt, rl);
+      for (int m = 0; m < nm; m++) {
+        mipo_reduced_pred(sd->size_id, m % sd->modes, m >= sd->modes, rt, rl, red);
+        const int16_t *p = red;
+        if (sd->size_id > 0) {
+          upsample(red, r, w, h, top, left, pred);
+          p = pred;
+        }
+        int a, b;
+        cu_distortion(orig, width, x, y, w, h, p, &a, &b);
+        cost[base + m] = 2 * a < b ? 2 * a : b; /* intra.cl:1166 */
+        if (sad) sad[base + m] = a;
+        if (satd) satd[base + m] = b;
+      }
+    }
+  }
+}
+
+void mipo_search_ctus(const uint16_t *orig, const uint16_t *refs, int width, int height,
+                      int ctu0, int ctu1, int32_t *cost, int32_t *sad, int32_t *satd,
+                      int nthreads) {
+#ifdef _OPENMP
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+  for (int c = ctu0; c < ctu1; c++) search_ctu(orig, refs, width, height, c, cost, sad, satd);
+  (void)nthreads;
+}
+
+void mipo_search_frame(const uint16_t *orig, const uint16_t *refs, int width, int height,
+                       int32_t *cost, int32_t *sad, int32_t *satd, int nthreads) {
+  mipo_search_ctus(orig, refs, width, height, 0, mipo_num_ctus(width, height), cost, sad,
+                   satd, nthreads);
+}
+
+void mipo_best_modes(const int32_t *cost, int nctus, uint8_t *best_mode, int32_t *best_cost) {
+  size_t cu_out = 0;
+  for (int c = 0; c < nctus; c++)
+    for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+      const mip_shape_desc *sd = &SHAPES[s];
+      const int nm = 2 * sd->modes;
+      for (int cu = 0; cu < sd->ncu; cu++, cu_out++) {
+        const int32_t *row = cost + (size_t)c * MIP_COSTS_PER_CTU + sd->cost_offset + (size_t)cu * nm;
+        int best = 0;
+        for (int m = 1; m < nm; m++)
+          if (row[m] < row[best]) best = m;
+        best_mode[cu_out] = row[best] == MIPO_UNAVAILABLE ? 0xff : (uint8_t)best;
+        if (best_cost) best_cost[cu_out] = row[best];
+      }
+    }
+}
+
+/* --------------------------------------------------------------------- filters --- */
+
+/* Validity of a tap at tile-relative (ty, tc) for the 2-D quarter-CTU kernels.  The
+ * tile is 128x32 at (qx, qy); gates restate the halo fetch conditions:
+ *   3x3: intra.cl:2903-2966, 5x5: intra.cl:3096-3189 (and the float twins).
+ * Interior taps are valid when inside the frame (the reference only tests the row;
+ * it assumes frame widths that are multiples of 128). */
+static int tap_valid(int ksz, int qx, int qy, int ty, int tc, int W, int H) {
+  const long long WH = (long long)W * H;
+  const long long g = (long long)(qy + ty) * W + qx + tc;
+  const int top = ty < 0, bot = ty >= 32, lft = tc < 0, rgt = tc >= 128;
+  if (!top && !bot && !lft && !rgt) return qy + ty < H && qx + tc < W;
+  if ((top || bot) && (lft || rgt)) { /* corners */
+    const int vy = top ? qy > 0 : qy + ty < H - 1;
+    const int vx = lft ? qx > 0 : qx + tc < W - 1;
+    return vy && vx;
+  }
+  if (top || bot) {
+    if (!(g > 0 && g < WH)) return 0;
+    if (ksz == 3) return 1;
+    return top ? qy > 0 : qy + ty + 2 < H - 1;
+  }
+  return g > 0 && g < WH && qx + tc > 0 && qx + tc < W - 1;
+}
+
+static void filter_2d(const uint16_t *in, uint16_t *out, int W, int H, const uint16_t *taps,
+                      int ksz, int is_float) {
+  const int rad = ksz / 2;
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      const int qx = x & ~127, qy = y & ~31;
+      int sum = 0, scale = 0;
+      for (int dy = -rad; dy <= rad; dy++)
+        for (int dx = -rad; dx <= rad; dx++) {
+          const int c = taps[(dy + rad) * ksz + dx + rad];
+          if (!tap_valid(ksz, qx, qy, y - qy + dy, x - qx + dx, W, H)) continue;
+          sum += c * in[(size_t)(y + dy) * W + x + dx];
+          scale += c;
+        }
+      int v;
+      if (is_float) v = (int)roundf((float)sum / (float)scale); /* intra.cl:1794, 2507 */
+      else v = (sum + scale / 2) / scale;                         /* intra.cl:3011, 3235 */
+      out[(size_t)y * W + x] = (uint16_t)v;
+    }
+}
+
+int mipo_filter_frame(const uint16_t *in, uint16_t *out, int width, int height, int filter,
+                      int kernel_idx) {
+  switch (filter) {
+    case MIPO_FILTER_2D_INT:
+    case MIPO_FILTER_2D_FLOAT:
+      if (kernel_idx < 0 || kernel_idx >= 5) return -1;
+      filter_2d(in, out, width, height, TAPS3 + 9 * kernel_idx, 3, filter == MIPO_FILTER_2D_FLOAT);
+      return 0;
+    case MIPO_FILTER_2D_INT_5x5:
+    case MIPO_FILTER_2D_FLOAT_5x5:
+      if (kernel_idx < 0 || kernel_idx >= 3) return -1;
+      filter_2d(in, out, width, height, TAPS5 + 25 * kernel_idx, 5,
+                filter == MIPO_FILTER_2D_FLOAT_5x5);
+      return 0;
+    default:
+      return -2; /* separable variants: see mipo_filter_frame_1d (not yet restated) */
+  }
+}
+
+/* ------------------------------------------------------------- synthetic frames --- */
+
+static uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* Integer-only generators so C and numpy (tests/synth.py) agree bit for bit.
+ * kind 0: smooth ramps + triangle-wave texture + per-32x32 DC offsets + noise (+-16);
+ * kind 1: uniform 10-bit noise. */
+void mipo_synth_frame(uint16_t *out, int width, int height, uint64_t seed, int kind) {
+  for (int y = 0; y < height; y++)
+    for (int x = 0; x < width; x++) {
+      const uint64_t h = splitmix64(seed * 0x100000001B3ull + (uint64_t)y * (uint64_t)width + (uint64_t)x);
+      int v;
+      if (kind == 1) {
+        v = (int)(h & 1023);
+      } else {
+        const uint64_t hb = splitmix64(seed ^ ((uint64_t)(y >> 5) << 32) ^ (uint64_t)(x >> 5));
+        const int ramp = ((x * 3 + y * 5) % 512);
+        const int tp = (x + 2 * y) % 96;
+        const int tri = (tp < 48 ? tp : 96 - tp) * 4;
+        const int dc = (int)(hb & 255) - 128;
+        const int noise = (int)((h >> 20) & 31) - 16;
+        v = 200 + ramp + tri - 96 + dc + noise;
+        v = v < 0 ? 0 : (v > 1023 ? 1023 : v);
+      }
+      out[(size_t)y * width + x] = (uint16_t)v;
+    }
+}

@@ -1,0 +1,57 @@
+// mip_kernels.h -- launch interface between the C-ABI host code (mipgpu.cpp) and the
+// gfx950 kernels (mip_search.hip, mip_filter.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mipgpu {
+
+// One wave-sized piece of work: 64 lanes of (CU, mode pair, 4-column strip) of one
+// CU shape, starting at job index `job0` (job = cu * modes + pair).
+struct WaveTask {
+  uint16_t shape;
+  uint16_t job0;
+};
+
+struct SearchArgs {
+  const uint16_t *orig;   // [frames][height][width] original samples (distortion)
+  const uint16_t *refs;   // reference-sample source: == orig, or the filtered frames
+  int32_t *cost;          // [frames][nctus][97840]  min(2*SAD, SATD)
+  int32_t *sad;           // optional, same layout
+  int32_t *satd;          // optional, same layout
+  const WaveTask *tasks;  // per-CTU wave-task list (heaviest first)
+  const int16_t *weights; // expanded MIP weights, see kWeightWords
+  int width, height;
+  int ctu_cols, nctus;
+  int ntasks;
+  int slices;             // workgroups per CTU
+};
+
+// Expanded weight table (int16): 16-byte rows of 8 taps, index (mode*outputs + j)*8.
+//   sizeId 2: rows [0, 384)    taps (0, w0..w6)   (mip_matrix.cl:441, intra.cl:459-463)
+//   sizeId 1: rows [384, 512)  taps w0..w7
+//   sizeId 0: rows [512, 768)  taps w0..w3, 0, 0, 0, 0
+constexpr int kWeightRowsS2 = 6 * 64, kWeightRowsS1 = 8 * 16, kWeightRowsS0 = 16 * 16;
+constexpr int kWeightRowOffS1 = kWeightRowsS2, kWeightRowOffS0 = kWeightRowsS2 + kWeightRowsS1;
+constexpr int kWeightWords = (kWeightRowsS2 + kWeightRowsS1 + kWeightRowsS0) * 8;
+
+struct BestArgs {
+  const int32_t *cost;
+  uint8_t *best_mode;
+  int32_t *best_cost;
+  int total_cus;          // frames * nctus * 5380
+};
+
+struct FilterArgs {
+  const uint16_t *in;
+  uint16_t *out;
+  int width, height, nframes;
+  int filter;             // reference whitelist index (constants.h:25-34)
+  int kernel_idx;
+};
+
+hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, hipStream_t s);
+hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
+hipError_t launch_filter(const FilterArgs &a, hipStream_t s);
+
+}  // namespace mipgpu
