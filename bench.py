@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench.py -- 1080p frames/s of the full MIP mode search over all 47 CU shapes.
+
+One *step* = one pass of the fused HIP search over a batch of B synthetic 1920x1080 frames
+resident in HBM (original references, BASELINE.json configs[1]), writing the complete
+int32 cost table (97840 entries per CTU, the reference's minSadHad table).  Frames shard
+across GPUs (one process per GPU, no data-path collective; RCCL only carries the barrier
+and the max-over-ranks of the timing) -> weak scaling.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints one JSON line (contract in the task statement), plus:
+  roofline      HBM roofline of the search kernel (algorithmic bytes = frame read + int32
+                cost write, per launch) with the launch time from HIP events on the stream
+                the kernel runs on, and the PMC-measured traffic when profiles/ holds it;
+  valu          the same launch priced in algorithmic integer ops (SURVEY.md section 8d
+                model, 140.3 M ops per CTU) against the VALU int32 rate -- the bound that
+                actually applies to this path;
+  cpu_baseline  the C oracle (oracle/mip_oracle.c, OpenMP) on the host cores, one full frame;
+  reference_gpu the reference's own OpenCL kernels (oracle/_ref, compiled from intra.cl)
+                timed on the same MI355X, when their code objects are present;
+  end_to_end    host-buffer API rate including PCIe transfers (never `value`).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "vvc-mip-gpu_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "1080p frames/sec, full MIP mode search over all CU sizes; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E peak (spec)
+VALU_PEAK_OPS = 256 * 128 * 2.4e9  # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz, int32 lane-ops/s
+OPS_PER_CTU = 140.3e6            # SURVEY.md section 8d algorithmic op model
+
+
+def dist_env():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def dist_max(value, world, device=None):
+    """Max over ranks (works for nccl with a device tensor and for gloo on CPU)."""
+    if world <= 1:
+        return value
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shard_seed(base_seed, rank):
+    """Each rank processes its own frames (frame sharding, no overlap)."""
+    return base_seed + 1000003 * rank
+
+
+def aggregate(frames_per_step, steps, world, max_elapsed_s):
+    total = frames_per_step * steps * world
+    return total / max_elapsed_s, 1000.0 * max_elapsed_s / steps
+
+
+def algorithmic_bytes_per_frame(w, h):
+    from mipgpu.layout import COSTS_PER_CTU, num_ctus
+    return w * h * 2 + num_ctus(w, h) * COSTS_PER_CTU * 4
+
+
+def load_traffic(width, height, frames):
+    """PMC-derived HBM bytes per launch for this workload, if a profile summary exists."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        key = "%dx%dx%d" % (width, height, frames)
+        return d.get(key, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(width, height, seed):
+    import numpy as np
+    import oracle_lib
+    from mipgpu.synth import synth_frame
+    threads = min(16, os.cpu_count() or 1)
+    frame = synth_frame(width, height, seed, 0)
+    oracle_lib.lib()
+    t0 = time.perf_counter()
+    oracle_lib.search(frame, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 4), "unit": "1080p frames/s" if (width, height) == (1920, 1080) else "frames/s",
+            "cores": threads, "kind": "port",
+            "sample": "1 synthetic %dx%d frame (all CTUs, full search) through the C oracle oracle/mip_oracle.c, "
+                      "OpenMP %d threads, %.2f s" % (width, height, threads, dt)}
+
+
+def reference_gpu(width, height, frames, seed):
+    runner = os.path.join(REPO, "oracle", "_ref", "ref_runner")
+    if not os.path.exists(runner):
+        return None
+    try:
+        out = subprocess.run([runner, "--bins", os.path.join(REPO, "oracle", "_ref"), "--width", str(width),
+                              "--height", str(height), "--frames", str(frames), "--synth", "0:%x" % seed,
+                              "--reps", "2"], capture_output=True, timeout=180, check=True).stdout.decode()
+        d = json.loads(out.strip().splitlines()[-1])
+        return {"value": round(1000.0 / d["device_ms_per_frame"], 2), "unit": "frames/s (device time)",
+                "wall_value": round(1000.0 / d["wall_ms_per_frame"], 2),
+                "kernel_ms_per_frame": d["kernel_ms"], "device": d["device"],
+                "note": "reference intra.cl kernels (initBoundaries, MIP_ReducedPred, 3x upsampleDistortion) "
+                        "compiled by the AMD OpenCL compiler, same GPU, same synthetic frames"}
+    except Exception as exc:  # the comparison is informative only
+        return {"error": str(exc)[:200]}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-step", type=int, default=8)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x1080)
+    ap.add_argument("--slices", type=int, default=0, help="workgroups per CTU (0 = engine default)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-reference-gpu", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from mipgpu import MipEngine
+    from mipgpu.layout import num_ctus
+    from mipgpu.synth import synth_frames
+
+    rank, local_rank, world = dist_env()
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    W, H, B = args.width, args.height, args.frames_per_step
+
+    host = synth_frames(W, H, B, shard_seed(args.seed, rank), 0)
+    frames = torch.from_numpy(host.astype(np.int16)).to(dev)
+    eng = MipEngine(W, H, device=local_rank, max_batch=B, slices_per_ctu=args.slices)
+    costs = torch.empty((B, eng.costs_per_frame), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        eng.search_device(frames, costs=costs, stream=stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        eng.search_device(frames, costs=costs, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one search launch per step, same stream
+
+    max_elapsed = dist_max(elapsed, world, dev)
+    max_kernel_ms = dist_max(kernel_ms, world, dev)
+    value, ms_per_step = aggregate(B, args.steps, world, max_elapsed)
+
+    if rank == 0:
+        alg_bytes = algorithmic_bytes_per_frame(W, H) * B
+        achieved = alg_bytes / (max_kernel_ms * 1e-3) / 1e9
+        ops = OPS_PER_CTU * num_ctus(W, H) * B
+        res = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16x2/int32",
+            "data": "synthetic (seeded integer generator, mipgpu/synth.py)",
+            "config": {"workload": "%dx%d frames, original references (BASELINE configs[1]); %d frames per step "
+                                   "per GPU resident in HBM; full int32 cost table written" % (W, H, B),
+                       "width": W, "height": H, "frames_per_step": B, "parallelism": "frames sharded over %d GPU(s)" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_traffic(W, H, B),
+                         "kernel": "mip_search_kernel", "kernel_ms_per_launch": round(max_kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "valu": {"achieved": round(ops / (max_kernel_ms * 1e-3) / 1e12, 3), "peak": round(VALU_PEAK_OPS / 1e12, 2),
+                     "unit": "Tops/s (algorithmic int ops, SURVEY 8d model)",
+                     "frac": round(ops / (max_kernel_ms * 1e-3) / VALU_PEAK_OPS, 4)},
+        }
+        if world == 1:
+            if not args.no_cpu_baseline:
+                res["cpu_baseline"] = cpu_baseline(W, H, args.seed)
+            # Host-buffer path incl. PCIe (pageable copies; informative, never `value`).
+            t0 = time.perf_counter()
+            for _ in range(2):
+                eng.search(host)
+            res["end_to_end"] = {"value": round(2 * B / (time.perf_counter() - t0), 2), "unit": "frames/s",
+                                 "note": "host frames in, host int32 cost tables out (H2D + search + D2H)"}
+            if not args.no_reference_gpu:
+                ref = reference_gpu(W, H, min(B, 4), args.seed)
+                if ref is not None:
+                    res["reference_gpu"] = ref
+                    if "value" in ref:
+                        res["speedup_vs_reference_gpu"] = round(value / ref["value"], 2)
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,124 @@
+/* mipgpu.h -- C ABI of the MI355X-native VVC MIP search engine (libmipgpu.so).
+ *
+ * Drop-in boundary for the hot path of iagostorch/VVC-MIP-GPU.  The reference has no
+ * FFI layer: its path is main.cpp's OpenCL dispatch of
+ *     filterFrame_<type>  (intra.cl:1639-3823, dispatched main.cpp:700-761)
+ *     initBoundaries      (intra.cl:17,   main.cpp:802-843)
+ *     MIP_ReducedPred     (intra.cl:349,  main.cpp:909-945)
+ *     upsampleDistortion  (intra.cl:545,  main.cpp:995-1199, built 3x with -DSIZEID)
+ * plus the cost read-back readMemobjsIntoArray_Distortion (main_aux_functions.h:585-630).
+ * Each entry point below replaces one of those steps (cited per function); the C++ CLI
+ * (vvc-mip-gpu_amd/cli/mipgpu_cli.cpp) replaces main.cpp on top of it.
+ *
+ * Conventions: plain pointers and sizes, int status (0 = ok, <0 = error, message via
+ * mip_last_error()), no exceptions cross the boundary.  Host buffers are owned by the
+ * caller; device buffers of the engine are owned by the engine.  One engine per device;
+ * an engine must be used by one host thread at a time.  Samples are 10-bit values in
+ * uint16; frames are row-major, consecutive frames are concatenated.
+ *
+ * Cost layout (identical to the reference's ALL_stridedDistortionsPerCtu,
+ * constants.h:1558-1631): int32 [frames][nCTUs][97840], entry
+ *     ctu*97840 + shape_offset + cu*2*modes + mode
+ * with the 47 CU shapes in reference order.  CUs that do not lie completely inside the
+ * frame are reported as MIP_COST_UNAVAILABLE (the reference leaves them undefined).
+ */
+#ifndef MIPGPU_H
+#define MIPGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIPGPU_ABI_VERSION 1
+#define MIP_COSTS_PER_CTU_ABI 97840
+#define MIP_CUS_PER_CTU_ABI 5380
+#define MIP_COST_UNAVAILABLE 0x7fffffff
+
+/* Reference filter whitelist order, constants.h:25-34. */
+typedef enum {
+  MIP_FILTER_NONE = -1,               /* USE_ALTERNATIVE_SAMPLES=0: references = originals */
+  MIP_FILTER_1D_INT = 0,              /* filterFrame_1d_int            intra.cl:3267 */
+  MIP_FILTER_1D_FLOAT = 1,            /* filterFrame_1d_float          intra.cl:1828 */
+  MIP_FILTER_2D_INT = 2,              /* filterFrame_2d_int_quarterCtu intra.cl:2856 */
+  MIP_FILTER_2D_FLOAT = 3,            /* filterFrame_2d_float_quarterCtu intra.cl:1639 */
+  MIP_FILTER_1D_INT_5x5 = 4,          /* filterFrame_1d_int_5x5        intra.cl:3508 */
+  MIP_FILTER_1D_FLOAT_5x5 = 5,        /* filterFrame_1d_float_5x5      intra.cl:2539 */
+  MIP_FILTER_2D_INT_5x5 = 6,          /* filterFrame_2d_int_5x5_quarterCtu intra.cl:3042 */
+  MIP_FILTER_2D_FLOAT_5x5 = 7         /* filterFrame_2d_float_5x5_quarterCtu intra.cl:2311 */
+} mip_filter_type;
+
+typedef struct {
+  int filter;          /* mip_filter_type; MIP_FILTER_NONE for original references */
+  int kernel_idx;      /* --KernelIdx: tap set index (0..4 for 3x3, 0..2 for 5x5) */
+  int max_batch;       /* frames per device batch (device buffers sized for this); >= 1 */
+  int want_sad_satd;   /* also produce the SAD / SATD tables (MAX_PERFORMANCE_DIST=0) */
+  int slices_per_ctu;  /* workgroups per CTU in the search kernel; 0 = auto */
+} mip_opts;
+
+typedef struct mip_engine mip_engine;
+
+/* Defaults: no filter, kernel_idx 0, max_batch 1, no SAD/SATD, auto slicing. */
+void mip_opts_default(mip_opts *opts);
+
+/* Create an engine on HIP device `device` for width x height frames (width, height
+ * multiples of 4).  Replaces main.cpp:90-598 (device/context/queue/buffer/program set-up).
+ * Returns 0 and *out, or <0. */
+int mip_engine_create(int device, int width, int height, const mip_opts *opts, mip_engine **out);
+int mip_engine_destroy(mip_engine *e);
+
+/* Geometry helpers. */
+int mip_num_ctus(int width, int height);                     /* intra.cl:31-33 */
+int64_t mip_costs_per_frame(int width, int height);          /* nCTUs * 97840 */
+int64_t mip_cus_per_frame(int width, int height);            /* nCTUs * 5380 */
+const char *mip_shape_name(int shape);                       /* main_aux_functions.h:296-401 */
+/* Geometry of CU shape `shape` (0..46): w, h, modes (without transposition), CU count per
+ * CTU, cost offset inside the CTU block.  Returns 0 or <0 for a bad index. */
+int mip_shape_info(int shape, int *w, int *h, int *modes, int *ncu, int *cost_offset);
+/* CTU-relative position of CU `cu` of `shape` (ALL_X_POS / ALL_Y_POS, constants.h:1235-1354). */
+int mip_cu_position(int shape, int cu, int *x, int *y);
+
+/* Low-pass filter of `nframes` host frames (filterFrame_<type>, main.cpp:700-761).
+ * out must hold nframes frames.  Synchronous. */
+int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int filter,
+                      int kernel_idx, uint16_t *out);
+
+/* Full MIP search of `nframes` (<= max_batch) host frames: H2D, [filter], search, D2H.
+ * Replaces the per-frame loop main.cpp:678-1241 + readMemobjsIntoArray_Distortion.
+ * refs_or_null: caller-provided reference-sample frames (alternative samples computed
+ * elsewhere); NULL = originals, or the engine's filter when opts.filter != NONE.
+ * costs_out: int32 [nframes][nCTUs*97840] (may be NULL if only best modes are wanted).
+ * best_mode_out / best_cost_out: optional per-CU argmin, [nframes][nCTUs*5380]
+ * (0xff / MIP_COST_UNAVAILABLE for unavailable CUs).
+ * sad_out / satd_out: optional (need opts.want_sad_satd).  Synchronous. */
+int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
+                      int nframes, int32_t *costs_out, uint8_t *best_mode_out,
+                      int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out);
+
+/* Device-resident variant (inputs already in HBM; all pointers are device pointers,
+ * `stream` is a hipStream_t or NULL for the engine stream).  Asynchronous on `stream`.
+ * d_refs NULL: originals, or the engine filter applied into engine scratch.
+ * d_costs required; the optional outputs may be NULL. */
+int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
+                      int nframes, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
+                      uint8_t *d_best_mode, int32_t *d_best_cost, void *stream);
+
+/* Device-resident filter (asynchronous on `stream`). */
+int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int height,
+                      int nframes, int filter, int kernel_idx, void *stream);
+
+/* Kernel-only timing of the search on resident buffers: runs `reps` launches of the
+ * fused search for `nframes` device frames, returns the mean device time per launch in
+ * milliseconds (HIP events on the engine stream), or <0. */
+double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
+                              int nframes, int32_t *d_costs, int reps);
+
+/* Last error message of the calling thread ("" if none). */
+const char *mip_last_error(void);
+int mip_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,65 @@
+"""C-ABI boundary: the library loads and exports exactly what include/mipgpu.h declares.
+Only host-side geometry helpers are called (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import mipgpu
+from mipgpu import layout
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "mipgpu.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mip_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(mipgpu.LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "vvc-mip-gpu_amd"), "lib/libmipgpu.so"])
+    return mipgpu.library()
+
+
+def test_exports_every_declared_symbol(lib):
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), s
+    out = subprocess.check_output(["nm", "-D", "--defined-only", mipgpu.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (mip_\w+)", out))
+    assert set(syms) <= exported
+
+
+def test_geometry_helpers(lib):
+    assert lib.mip_abi_version() == 1
+    assert lib.mip_num_ctus(1920, 1080) == 135
+    assert lib.mip_num_ctus(3840, 2160) == 510
+    assert lib.mip_num_ctus(7680, 4320) == 2040
+    assert lib.mip_costs_per_frame(1920, 1080) == 135 * 97840
+    assert lib.mip_cus_per_frame(1920, 1080) == 135 * 5380
+    for s in layout.SHAPES:
+        assert lib.mip_shape_name(s.index).decode() == s.name
+        w, h, m, n, o = (ctypes.c_int() for _ in range(5))
+        assert lib.mip_shape_info(s.index, *(ctypes.byref(v) for v in (w, h, m, n, o))) == 0
+        assert (w.value, h.value, m.value, n.value, o.value) == (s.w, s.h, s.modes, s.ncu, s.cost_offset)
+        xs, ys = s.positions()
+        for cu in (0, s.ncu // 2, s.ncu - 1):
+            x, y = ctypes.c_int(), ctypes.c_int()
+            assert lib.mip_cu_position(s.index, cu, ctypes.byref(x), ctypes.byref(y)) == 0
+            assert (x.value, y.value) == (xs[cu], ys[cu])
+    assert lib.mip_shape_info(47, None, None, None, None, None) != 0
+    assert b"bad shape" in lib.mip_last_error()
+
+
+def test_filter_names_follow_reference_whitelist():
+    assert mipgpu.filter_index("filterFrame_2d_float_5x5_quarterCtu") == 7
+    assert mipgpu.filter_index(None) == mipgpu.FILTER_NONE
+    with pytest.raises(mipgpu.MipError):
+        mipgpu.filter_index("filterFrame_2d")  # half-CTU kernel, not whitelisted (constants.h:25-34)

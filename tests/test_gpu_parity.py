@@ -1,0 +1,121 @@
+"""HIP path parity: libmipgpu.so (gfx950 kernels) against the C oracle and against the
+reference kernels' golden outputs.  Integer path -> bit-exact everywhere; the float
+filters are also required to be bit-exact (tolerance 0: correctly rounded fp32 division
+makes round(sum/scale) equal the integer rounding, and the reference agreed on every
+fixture)."""
+import numpy as np
+import pytest
+
+import golden_utils as G
+import oracle_lib as O
+from mipgpu import MipEngine, MipError, filter_index, layout
+from mipgpu.synth import synth_frame, synth_frames
+
+pytestmark = pytest.mark.gpu
+
+FILTERS_2D = [("filterFrame_2d_int_quarterCtu", 5), ("filterFrame_2d_float_quarterCtu", 5),
+              ("filterFrame_2d_int_5x5_quarterCtu", 3), ("filterFrame_2d_float_5x5_quarterCtu", 3)]
+
+
+def _engine(c, **kw):
+    return MipEngine(c["width"], c["height"], filter=c["filter"], kernel_idx=c["kernel_idx"],
+                     max_batch=c["frames"], **kw)
+
+
+@pytest.mark.parametrize("name", [n for n in G.names() if n.startswith("small_")])
+def test_small_configs_vs_oracle_and_reference(gpu_available, name):
+    fx = G.load(name)
+    c = fx["config"]
+    frames = G.inputs(fx)
+    with _engine(c, want_sad_satd=True) as eng:
+        out = eng.search(frames, sad_satd=True)
+    for f, fr in enumerate(fx["frames"]):
+        refs = O.filter_frame(frames[f], c["filter"], c["kernel_idx"]) if c["filter"] else None
+        oc, osad, osatd = O.search(frames[f], refs, want_sad_satd=True)
+        assert np.array_equal(out["cost"][f], oc)
+        assert np.array_equal(out["sad"][f], osad)
+        assert np.array_equal(out["satd"][f], osatd)
+        assert G.sha(G.masked(out["cost"][f], c["width"], c["height"])) == fr["cost_sha256"]
+        if "sad_sha256" in fr:
+            assert G.sha(G.masked(out["sad"][f], c["width"], c["height"])) == fr["sad_sha256"]
+            assert G.sha(G.masked(out["satd"][f], c["width"], c["height"])) == fr["satd_sha256"]
+
+
+@pytest.mark.parametrize("name", [n for n in G.names() if not n.startswith("small_")])
+def test_full_size_configs_vs_reference(gpu_available, name):
+    """1080p / 4K: the whole masked cost table hashes to the reference's."""
+    fx = G.load(name)
+    c = fx["config"]
+    frames = G.inputs(fx)
+    with _engine(c) as eng:
+        out = eng.search(frames)
+        if c["filter"]:
+            filt = eng.filter_frames(frames, c["filter"], c["kernel_idx"])
+    for f, fr in enumerate(fx["frames"]):
+        assert G.sha(G.masked(out["cost"][f], c["width"], c["height"])) == fr["cost_sha256"]
+        for ctu in map(int, fr["ctu_rows"]):
+            row = out["cost"][f][ctu * 97840:(ctu + 1) * 97840]
+            m = layout.available_mask(c["width"], c["height"])[ctu * 97840:(ctu + 1) * 97840]
+            assert np.array_equal(np.where(m, row, layout.UNAVAILABLE), G.ctu_row(fx, f, ctu))
+        if c["filter"]:
+            assert G.sha(filt[f]) == fr["filtered_sha256"]
+
+
+@pytest.mark.parametrize("filt,nk", FILTERS_2D)
+def test_filters_vs_oracle(gpu_available, filt, nk):
+    frame = synth_frame(392, 136, 0x51, 1)  # partial tiles on both axes
+    with MipEngine(392, 136) as eng:
+        for k in range(nk):
+            got = eng.filter_frames(frame, filt, k)[0]
+            assert np.array_equal(got, O.filter_frame(frame, filt, k)), (filt, k)
+
+
+@pytest.mark.parametrize("w,h,kind", [(136, 72, 0), (8, 8, 1), (132, 260, 1), (128, 4, 0), (640, 384, 1)])
+def test_edge_frame_sizes(gpu_available, w, h, kind):
+    frame = synth_frame(w, h, 0x77 + w + h, kind)
+    with MipEngine(w, h, want_sad_satd=True) as eng:
+        out = eng.search(frame, sad_satd=True, best=True)
+    oc, osad, osatd = O.search(frame, want_sad_satd=True)
+    assert np.array_equal(out["cost"][0], oc)
+    assert np.array_equal(out["sad"][0], osad)
+    assert np.array_equal(out["satd"][0], osatd)
+    bm, bc = layout.best_modes(oc, layout.num_ctus(w, h))
+    assert np.array_equal(out["best_mode"][0], bm)
+    assert np.array_equal(out["best_cost"][0], bc)
+    avail = layout.available_mask(w, h)
+    assert (oc[~avail] == layout.UNAVAILABLE).all()
+
+
+def test_alt_refs_supplied_by_caller(gpu_available):
+    frame = synth_frame(256, 136, 0x99, 0)
+    refs = synth_frame(256, 136, 0x9A, 1)
+    with MipEngine(256, 136) as eng:
+        out = eng.search(frame, refs=refs)
+    assert np.array_equal(out["cost"][0], O.search(frame, refs))
+
+
+def test_batched_device_api_matches_host_api(gpu_available):
+    import torch
+    w, h, n = 384, 256, 3
+    frames = synth_frames(w, h, n, 0x123, 0)
+    with MipEngine(w, h, max_batch=n, filter="filterFrame_2d_float_5x5_quarterCtu", kernel_idx=2) as eng:
+        host = eng.search(frames, best=True)
+        d = torch.from_numpy(frames.astype(np.int16)).cuda()
+        costs = eng.search_device(d)
+        bm = torch.empty((n, eng.cus_per_frame), dtype=torch.uint8, device="cuda")
+        eng.search_device(d, costs=costs, best_mode=bm)
+        torch.cuda.synchronize()
+        assert np.array_equal(costs.cpu().numpy(), host["cost"])
+        assert np.array_equal(bm.cpu().numpy(), host["best_mode"])
+    for f in range(n):
+        refs = O.filter_frame(frames[f], "filterFrame_2d_float_5x5_quarterCtu", 2)
+        assert np.array_equal(host["cost"][f], O.search(frames[f], refs))
+
+
+def test_errors_are_loud(gpu_available):
+    with pytest.raises(MipError):
+        MipEngine(130, 64)  # width not a multiple of 4
+    with pytest.raises(MipError):
+        MipEngine(128, 64, filter="filterFrame_2d_int_quarterCtu", kernel_idx=7)
+    with pytest.raises(MipError):
+        filter_index("filterFrame_2d_float")  # not whitelisted

@@ -1,0 +1,64 @@
+"""Static tables: the generated header / Python table vs the reference's constants."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from mipgpu import layout
+
+REF = "/root/reference"
+HAVE_REF = os.path.exists(os.path.join(REF, "constants.cl"))
+TOOLS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools")
+
+
+def test_cost_layout_totals():
+    assert sum(s.ncu * s.total_modes for s in layout.SHAPES) == layout.COSTS_PER_CTU == 97840
+    assert sum(s.ncu for s in layout.SHAPES) == layout.CUS_PER_CTU == 5380
+    offs = [s.cost_offset for s in layout.SHAPES]
+    assert offs == sorted(offs) and offs[0] == 0
+
+
+def test_cu_positions_inside_ctu_and_disjoint():
+    for s in layout.SHAPES:
+        x, y = s.positions()
+        assert (x % 4 == 0).all() and (y % 4 == 0).all()
+        assert (x + s.w <= 128).all() and (y + s.h <= 128).all()
+        occ = np.zeros((128, 128), np.int32)
+        for xi, yi in zip(x, y):
+            occ[yi:yi + s.h, xi:xi + s.w] += 1
+        assert occ.max() == 1, s.name  # CUs of one shape never overlap
+
+
+def test_best_modes_numpy():
+    rng = np.random.default_rng(1)
+    c = rng.integers(0, 1000, size=2 * 97840).astype(np.int32)
+    c[5] = layout.UNAVAILABLE
+    m, v = layout.best_modes(c, 2)
+    assert m.shape == (2 * 5380,)
+    s0 = layout.SHAPES[0]
+    row = c[:s0.total_modes]
+    assert m[0] == np.argmin(row) and v[0] == row.min()
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="reference tree not mounted")
+def test_generated_header_matches_reference():
+    """Re-derive the tables from the reference files and compare with the committed ones."""
+    sys.path.insert(0, TOOLS)
+    from gen_tables import render
+    text, offs, c = render()
+    hdr = os.path.join(os.path.dirname(TOOLS), "vvc-mip-gpu_amd", "csrc", "mip_tables.h")
+    assert open(hdr).read() == text
+    assert offs + [97840] == c["ALL_stridedDistortionsPerCtu"]
+    # Positions re-expanded from the lattice description == ALL_X_POS / ALL_Y_POS rows.
+    from refparse import parse_rows
+    X = parse_rows(REF + "/constants.cl", "ALL_X_POS")
+    Y = parse_rows(REF + "/constants.cl", "ALL_Y_POS")
+    for s in layout.SHAPES[:46]:
+        x, y = s.positions()
+        assert list(x) == X[s.index][:s.ncu] and list(y) == Y[s.index][:s.ncu], s.name
+    assert [s.w for s in layout.SHAPES] == c["ALL_widths"]
+    assert [s.h for s in layout.SHAPES] == c["ALL_heights"]
+    assert [s.ncu for s in layout.SHAPES] == c["ALL_cusPerCtu"]
+    assert [s.modes for s in layout.SHAPES] == c["ALL_numPredModes"]

@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, bench, kernel-trace profile.  Every GPU step has
+# its own time limit and the chain stops at the first failure.
+set -euo pipefail
+cd "$(dirname "$0")/.."
+OUT=${OUT:-gpurun_out}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() { echo "== $1 $(date +%T)"; }
+step pytest
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
+tail -3 "$OUT/pytest_gpu.log"
+step smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 1; }
+cat "$OUT/smoke.log"
+step bench
+timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+cat "$OUT/bench.json"
+step rocprof
+rm -rf "$OUT/prof"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+  python bench.py --no-cpu-baseline --no-reference-gpu --steps 10 > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
+  || { tail -20 "$OUT/prof.err"; exit 1; }
+find "$OUT/prof" -name "*stats*" | head
+step done

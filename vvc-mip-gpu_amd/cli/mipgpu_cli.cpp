@@ -1,0 +1,345 @@
+// mipgpu_cli.cpp -- command-line front end replacing the reference's main.cpp.
+//
+// Same flags as main.cpp:51-59 (boost::program_options style, including unambiguous
+// long-option prefixes such as --Filter=...):
+//   -h/--help  --DeviceIndex N  -f/--FramesToBeEncoded N  -s/--Resolution WxH
+//   -o/--OriginalFrames file.csv  -l/--OutputPreffix prefix  --FilterType name  --KernelIdx K
+// Same input format (CSV: H lines of W comma-separated samples per frame, frames
+// concatenated, main.cpp:364-384), same cost log (<prefix>.csv, header
+// "CTU,cuSizeName,W,H,CU,X,Y,Mode,SAD,SATD,minSadHad", one row per (CTU, shape, CU, mode)
+// for frame 0, main_aux_functions.h:735-798) and the same timing line
+// ("Elapsed time (ms) from writing samples to reading distortion (Nx), T",
+// main_aux_functions.h:908-914).  In the reference's default build
+// (MAX_PERFORMANCE_DIST=1) the SAD/SATD columns print never-written memory (0 in
+// practice); this CLI prints 0 there too unless --ReportSadSatd is given.
+// Extensions: --ReportSadSatd, --AllFrames (log every frame, column CTU stays per frame,
+// a Frame column is NOT added to keep the format), --BestModes file (per-CU decision),
+// --BatchFrames N, --Threads N (log formatting threads).
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mipgpu.h"
+
+namespace {
+
+const char *kFilters[] = {"filterFrame_1d_int", "filterFrame_1d_float", "filterFrame_2d_int_quarterCtu",
+                          "filterFrame_2d_float_quarterCtu", "filterFrame_1d_int_5x5", "filterFrame_1d_float_5x5",
+                          "filterFrame_2d_int_5x5_quarterCtu", "filterFrame_2d_float_5x5_quarterCtu"};
+
+struct Options {
+  int device = 0, frames = -1, kernel_idx = 0, batch = 8, threads = 0;
+  bool device_set = false, prefix_set = false, kidx_set = false, help = false;
+  bool sad_satd = false, all_frames = false;
+  std::string resolution, input, prefix, filter, best_modes;
+};
+
+struct OptDef {
+  const char *name;
+  char shortname;
+  bool takes_value;
+};
+const OptDef kOpts[] = {{"help", 'h', false},        {"DeviceIndex", 0, true},   {"FramesToBeEncoded", 'f', true},
+                        {"Resolution", 's', true},   {"OriginalFrames", 'o', true}, {"OutputPreffix", 'l', true},
+                        {"FilterType", 0, true},     {"KernelIdx", 0, true},     {"ReportSadSatd", 0, false},
+                        {"AllFrames", 0, false},     {"BestModes", 0, true},     {"BatchFrames", 0, true},
+                        {"Threads", 0, true}};
+
+void usage() {
+  std::cout << "Allowed options:\n"
+               "  -h [ --help ]                     produce help message\n"
+               "  --DeviceIndex arg (=0)            Index of the GPU device\n"
+               "  -f [ --FramesToBeEncoded ] arg    Number of frames to be processed\n"
+               "  -s [ --Resolution ] arg           Resolution of the video, in the format 1920x1080\n"
+               "  -o [ --OriginalFrames ] arg       Input file for original frames samples\n"
+               "  -l [ --OutputPreffix ] arg (=\"\")  Output files preffix with produced costs\n"
+               "  --FilterType arg                  Type of smoothing filter\n"
+               "  --KernelIdx arg (=0)              Index of the filtering kernel used to define the coefficients\n"
+               "  --ReportSadSatd                   Log real SAD/SATD columns (reference: MAX_PERFORMANCE_DIST=0)\n"
+               "  --AllFrames                       Log every frame (reference logs frame 0 only)\n"
+               "  --BestModes arg                   Write the per-CU best mode / cost to this CSV\n"
+               "  --BatchFrames arg (=8)            Frames per device batch\n"
+               "  --Threads arg (=0)                Log-formatting threads (0 = all cores)\n";
+}
+
+int set_opt(Options &o, const std::string &name, const std::string &val) {
+  try {
+    if (name == "help") o.help = true;
+    else if (name == "DeviceIndex") o.device = std::stoi(val), o.device_set = true;
+    else if (name == "FramesToBeEncoded") o.frames = std::stoi(val);
+    else if (name == "Resolution") o.resolution = val;
+    else if (name == "OriginalFrames") o.input = val;
+    else if (name == "OutputPreffix") o.prefix = val, o.prefix_set = true;
+    else if (name == "FilterType") o.filter = val;
+    else if (name == "KernelIdx") o.kernel_idx = std::stoi(val), o.kidx_set = true;
+    else if (name == "ReportSadSatd") o.sad_satd = true;
+    else if (name == "AllFrames") o.all_frames = true;
+    else if (name == "BestModes") o.best_modes = val;
+    else if (name == "BatchFrames") o.batch = std::max(1, std::stoi(val));
+    else if (name == "Threads") o.threads = std::stoi(val);
+  } catch (...) {
+    std::cerr << "the argument ('" << val << "') for option '--" << name << "' is invalid\n";
+    return 1;
+  }
+  return 0;
+}
+
+// boost-like parsing: --name=value, --name value, unambiguous prefixes, -x value, -xvalue.
+int parse(int argc, char **argv, Options &o) {
+  for (int i = 1; i < argc; i++) {
+    std::string a = argv[i], name, val;
+    bool have_val = false;
+    const OptDef *def = nullptr;
+    if (a.rfind("--", 0) == 0) {
+      std::string body = a.substr(2);
+      const size_t eq = body.find('=');
+      if (eq != std::string::npos) val = body.substr(eq + 1), body = body.substr(0, eq), have_val = true;
+      std::vector<const OptDef *> hits;
+      for (const OptDef &d : kOpts) {
+        if (body == d.name) { hits = {&d}; break; }
+        if (std::string(d.name).rfind(body, 0) == 0) hits.push_back(&d);
+      }
+      if (hits.size() != 1) {
+        std::cerr << (hits.empty() ? "unrecognised option '" : "option '") << a
+                  << (hits.empty() ? "'\n" : "' is ambiguous\n");
+        return 1;
+      }
+      def = hits[0];
+    } else if (a.size() >= 2 && a[0] == '-') {
+      for (const OptDef &d : kOpts)
+        if (d.shortname == a[1]) def = &d;
+      if (!def) { std::cerr << "unrecognised option '" << a << "'\n"; return 1; }
+      if (a.size() > 2) val = a.substr(2), have_val = true;
+    } else {
+      std::cerr << "unexpected positional argument '" << a << "'\n";
+      return 1;
+    }
+    if (def->takes_value && !have_val) {
+      if (i + 1 >= argc) { std::cerr << "the required argument for option '--" << def->name << "' is missing\n"; return 1; }
+      val = argv[++i];
+    }
+    if (set_opt(o, def->name, val)) return 1;
+  }
+  return 0;
+}
+
+// main_aux_functions.h:113-162
+int report_parameters(const Options &o, bool alt) {
+  int errors = 0;
+  std::cout << "-=-= INPUT PARAMETERS =-=-" << std::endl;
+  if (!o.device_set) std::cout << "  Device index not set. Using standard value of " << o.device << "." << std::endl;
+  else std::cout << "  Device Index=" << o.device << std::endl;
+  if (!o.prefix_set) std::cout << "  OutputPreffix log file not set. The output will not be written to any file." << std::endl;
+  else std::cout << "  OutputPreffix=" << o.prefix << std::endl;
+  if (o.frames >= 0) std::cout << "  FramesToBeEncoded=" << o.frames << std::endl;
+  else { std::cout << "  [!] ERROR: FramesToBeEncoded not set." << std::endl; errors++; }
+  if (!o.input.empty()) std::cout << "  InputOriginalFrame=" << o.input << std::endl;
+  else { std::cout << "  [!] ERROR: Input original frames not set." << std::endl; errors++; }
+  if (alt) {
+    std::cout << "  FilterType=" << o.filter << std::endl;
+    if (!o.kidx_set) std::cout << "  KernelIdx not set. Using default value zero." << std::endl;
+    else std::cout << "  KernelIdx=" << o.kernel_idx << std::endl;
+  }
+  return errors;
+}
+
+// Fast CSV reader (main.cpp:364-384 format).
+bool read_frames(const std::string &path, int W, int H, int n, std::vector<uint16_t> &out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  out.assign((size_t)W * H * n, 0);
+  const char *p = data.c_str(), *end = p + data.size();
+  for (size_t row = 0; row < (size_t)H * n; row++) {
+    for (int x = 0; x < W; x++) {
+      while (p < end && (*p == ' ' || *p == '\r')) p++;
+      int v = 0;
+      bool any = false;
+      while (p < end && *p >= '0' && *p <= '9') v = v * 10 + (*p++ - '0'), any = true;
+      if (!any) return false;
+      out[row * W + x] = (uint16_t)v;
+      while (p < end && *p != ',' && *p != '\n') p++;
+      if (p < end && *p == ',') p++;
+    }
+    while (p < end && *p != '\n') p++;
+    if (p < end) p++;
+  }
+  return true;
+}
+
+inline char *put_int(char *p, long long v) {
+  char tmp[24];
+  int n = 0;
+  const bool neg = v < 0;
+  unsigned long long u = neg ? (unsigned long long)(-v) : (unsigned long long)v;
+  do tmp[n++] = (char)('0' + u % 10); while (u /= 10);
+  if (neg) *p++ = '-';
+  while (n) *p++ = tmp[--n];
+  return p;
+}
+
+struct ShapeInfo {
+  int w, h, modes, ncu, off;
+  std::string name;
+  std::vector<int> x, y;
+};
+
+// exportAllDistortionValues_File (main_aux_functions.h:735-798), formatted by CTU chunks
+// in parallel and written in order.
+void write_cost_log(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, int W, const int32_t *cost,
+                    const int32_t *sad, const int32_t *satd, int threads) {
+  const int ctu_cols = (W + 127) / 128;
+  const int chunk = 8;
+  const int nchunks = (nctus + chunk - 1) / chunk;
+  std::vector<std::string> bufs(nchunks);
+  auto work = [&](int c) {
+    std::string &s = bufs[c];
+    s.resize((size_t)chunk * MIP_COSTS_PER_CTU_ABI * 80);
+    char *p = &s[0];
+    for (int ctu = c * chunk; ctu < std::min(nctus, (c + 1) * chunk); ctu++) {
+      const int cx = 128 * (ctu % ctu_cols), cy = 128 * (ctu / ctu_cols);
+      for (const ShapeInfo &sh : shapes)
+        for (int cu = 0; cu < sh.ncu; cu++)
+          for (int m = 0; m < 2 * sh.modes; m++) {
+            const size_t idx = (size_t)ctu * MIP_COSTS_PER_CTU_ABI + sh.off + (size_t)cu * 2 * sh.modes + m;
+            p = put_int(p, ctu); *p++ = ',';
+            memcpy(p, sh.name.data(), sh.name.size()); p += sh.name.size(); *p++ = ',';
+            p = put_int(p, sh.w); *p++ = ',';
+            p = put_int(p, sh.h); *p++ = ',';
+            p = put_int(p, cu); *p++ = ',';
+            p = put_int(p, cx + sh.x[cu]); *p++ = ',';
+            p = put_int(p, cy + sh.y[cu]); *p++ = ',';
+            p = put_int(p, m); *p++ = ',';
+            p = put_int(p, sad ? sad[idx] : 0); *p++ = ',';
+            p = put_int(p, satd ? satd[idx] : 0); *p++ = ',';
+            p = put_int(p, cost[idx]); *p++ = '\n';
+          }
+    }
+    s.resize(p - &s[0]);
+  };
+  const int nt = std::max(1, threads);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; t++)
+    pool.emplace_back([&, t] {
+      for (int c = t; c < nchunks; c += nt) work(c);
+    });
+  for (auto &th : pool) th.join();
+  for (const std::string &s : bufs) fwrite(s.data(), 1, s.size(), fp);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  Options o;
+  if (parse(argc, argv, o)) return 1;
+  if (o.help) { usage(); return 1; }  // main.cpp:64-67 returns 1 after help
+  const bool alt = !o.filter.empty();
+  const int errors = report_parameters(o, alt);
+  int filter = MIP_FILTER_NONE;
+  if (alt) {
+    for (int i = 0; i < 8; i++)
+      if (o.filter == kFilters[i]) filter = i;
+    if (filter == MIP_FILTER_NONE) {
+      std::cout << "  [!] ERROR: Filter type " << o.filter << " not supported" << std::endl;
+      return 0;  // main.cpp:74-76 exits with 0
+    }
+  }
+  if (errors > 0) {
+    std::cout << "Exiting after finding errors in input parameters" << std::endl;
+    return 1;
+  }
+  int W = 0, H = 0;
+  if (sscanf(o.resolution.c_str(), "%dx%d", &W, &H) != 2 || W <= 0 || H <= 0) {
+    std::cout << "  [!] ERROR: Input resolution \"" << o.resolution << "\" not set properly" << std::endl;
+    return 0;
+  }
+  std::vector<uint16_t> frames;
+  if (!read_frames(o.input, W, H, o.frames, frames)) {
+    perror("error while opening samples files");
+    return 1;
+  }
+  const int nctus = mip_num_ctus(W, H);
+  mip_opts opts;
+  mip_opts_default(&opts);
+  opts.filter = filter;
+  opts.kernel_idx = o.kernel_idx;
+  opts.max_batch = std::min(o.batch, std::max(1, o.frames));
+  opts.want_sad_satd = o.sad_satd ? 1 : 0;
+  mip_engine *e = nullptr;
+  if (mip_engine_create(o.device, W, H, &opts, &e) != 0) {
+    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
+    return 1;
+  }
+  const size_t cpf = (size_t)nctus * MIP_COSTS_PER_CTU_ABI, upf = (size_t)nctus * MIP_CUS_PER_CTU_ABI;
+  std::vector<int32_t> cost(cpf * o.frames), sad, satd, best_cost;
+  std::vector<uint8_t> best;
+  if (o.sad_satd) sad.resize(cost.size()), satd.resize(cost.size());
+  if (!o.best_modes.empty()) best.resize(upf * o.frames), best_cost.resize(upf * o.frames);
+
+  const auto t0 = std::chrono::steady_clock::now();  // save_startTime, main.cpp:568
+  const int rc = mip_search_frames(e, frames.data(), nullptr, o.frames, cost.data(),
+                                   best.empty() ? nullptr : best.data(), best.empty() ? nullptr : best_cost.data(),
+                                   o.sad_satd ? sad.data() : nullptr, o.sad_satd ? satd.data() : nullptr);
+  const auto t1 = std::chrono::steady_clock::now();  // save_finishTime, main.cpp:1249
+  if (rc != 0) {
+    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
+    mip_engine_destroy(e);
+    return 1;
+  }
+  for (int f = 0; f < o.frames; f++) std::cout << "Current frame " << f << std::endl;
+
+  std::vector<ShapeInfo> shapes(47);
+  for (int s = 0; s < 47; s++) {
+    ShapeInfo &sh = shapes[s];
+    mip_shape_info(s, &sh.w, &sh.h, &sh.modes, &sh.ncu, &sh.off);
+    sh.name = mip_shape_name(s);
+    sh.x.resize(sh.ncu);
+    sh.y.resize(sh.ncu);
+    for (int cu = 0; cu < sh.ncu; cu++) mip_cu_position(s, cu, &sh.x[cu], &sh.y[cu]);
+  }
+  const int threads = o.threads > 0 ? o.threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  // reportDistortionToFile=1 in the reference even when -l is not given (writes ".csv").
+  {
+    FILE *fp = fopen((o.prefix + ".csv").c_str(), "w");
+    if (!fp) { perror("cannot open cost log"); mip_engine_destroy(e); return 1; }
+    fprintf(fp, "CTU,cuSizeName,W,H,CU,X,Y,Mode,SAD,SATD,minSadHad\n");
+    const int nlog = o.all_frames ? o.frames : std::min(1, o.frames);
+    for (int f = 0; f < nlog; f++)
+      write_cost_log(fp, shapes, nctus, W, cost.data() + f * cpf, o.sad_satd ? sad.data() + f * cpf : nullptr,
+                     o.sad_satd ? satd.data() + f * cpf : nullptr, threads);
+    fclose(fp);
+  }
+  if (!o.best_modes.empty()) {
+    FILE *fp = fopen(o.best_modes.c_str(), "w");
+    if (!fp) { perror("cannot open best-mode file"); mip_engine_destroy(e); return 1; }
+    fprintf(fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,Transposed,Cost\n");
+    const int ctu_cols = (W + 127) / 128;
+    for (int f = 0; f < o.frames; f++)
+      for (int ctu = 0, k = 0; ctu < nctus; ctu++)
+        for (const ShapeInfo &sh : shapes)
+          for (int cu = 0; cu < sh.ncu; cu++, k++) {
+            const size_t i = f * upf + (size_t)ctu * MIP_CUS_PER_CTU_ABI + (k % MIP_CUS_PER_CTU_ABI);
+            const int m = best[i];
+            fprintf(fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu,
+                    128 * (ctu % ctu_cols) + sh.x[cu], 128 * (ctu / ctu_cols) + sh.y[cu], m == 0xff ? -1 : m % sh.modes,
+                    m == 0xff ? -1 : (m >= sh.modes), best_cost[i]);
+          }
+    fclose(fp);
+  }
+  const long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count();
+  printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n");
+  printf("TIMING RESULTS (miliseconds)\n");
+  printf("Elapsed time (ms) from writing samples to reading distortion (%dx), %ld\n", o.frames, ms);
+  printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n\n");
+  mip_engine_destroy(e);
+  return 0;
+}

@@ -31,6 +31,13 @@ typedef short __attribute__((ext_vector_type(2))) s2;
 typedef unsigned short __attribute__((ext_vector_type(2))) u2;
 
 __constant__ mip_shape_desc c_shapes[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;
+// Size class of each shape (index into the run_task<W, H> instantiations below).
+__constant__ uint8_t c_shape_class[MIP_NUM_SHAPES] = {
+    0, 1, 2, 3, 4, 5, 6, 7, 8,                                  // aligned SizeId 2
+    2, 3, 4, 4, 5, 5, 6, 6, 6, 7, 7, 7, 7, 7, 8, 8, 8, 8, 8,    // NA SizeId 2
+    9, 10, 11, 12, 13, 14, 14, 15, 15,                          // aligned SizeId 1
+    11, 12, 13, 13, 13, 13, 13, 14, 15,                         // NA SizeId 1
+    16};                                                        // 4x4
 
 constexpr int kPitch = 132;   // LDS row pitch in samples: 66 dwords, rows rotate banks by 2
 constexpr int kColOff = 4;    // LDS column of CTU column 0 (columns -4..-1 hold the left halo)
@@ -146,37 +153,33 @@ __device__ __forceinline__ void anchor_row(const Lane<W, H> &L, int k, int x0, i
 // the seven non-DC pair maxima and U = |AC0| + (|DC| >> 2):  satd = T + ((U + 1) >> 1).
 // By Parseval (||c||_2 = 4 ||d||_2) satd <= 32736 and T <= satd, so u16 holds both.
 // SAD = sum |d| = 2 * sum max(d, 0) - DC, exact in 16 bits for the same reason.
-__device__ __forceinline__ void block_distortion(const s2 (&pred)[16], const uint2 (&orow)[4],
-                                                 uint32_t &sad0, uint32_t &sad1,
-                                                 uint32_t &satd0, uint32_t &satd1) {
-  s2 d[16];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const s2 o01 = as_s2(orow[i].x), o23 = as_s2(orow[i].y);
-    d[4 * i + 0] = s2{o01.x, o01.x} - pred[4 * i + 0];
-    d[4 * i + 1] = s2{o01.y, o01.y} - pred[4 * i + 1];
-    d[4 * i + 2] = s2{o23.x, o23.x} - pred[4 * i + 2];
-    d[4 * i + 3] = s2{o23.y, o23.y} - pred[4 * i + 3];
-  }
-  s2 pos = smax(d[0], splat(0));
-#pragma unroll
-  for (int i = 1; i < 16; i++) pos += smax(d[i], splat(0));
+struct BlockAcc {
+  s2 t[16];  // row-transformed residual
+  s2 pos;    // sum of max(d, 0)
+};
 
-  s2 t[16];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const s2 s0 = d[4 * i] + d[4 * i + 1], s1 = d[4 * i] - d[4 * i + 1];
-    const s2 s2_ = d[4 * i + 2] + d[4 * i + 3], s3 = d[4 * i + 2] - d[4 * i + 3];
-    t[4 * i + 0] = s0 + s2_;
-    t[4 * i + 1] = s1 + s3;
-    t[4 * i + 2] = s0 - s2_;
-    t[4 * i + 3] = s1 - s3;
-  }
+// One residual row of a 4x4 block: d = orig - pred, positive-part sum, row butterflies.
+__device__ __forceinline__ void block_row(BlockAcc &b, int i, const s2 (&prow)[4], uint2 orow) {
+  const s2 o01 = as_s2(orow.x), o23 = as_s2(orow.y);
+  const s2 d0 = s2{o01.x, o01.x} - prow[0], d1 = s2{o01.y, o01.y} - prow[1];
+  const s2 d2 = s2{o23.x, o23.x} - prow[2], d3 = s2{o23.y, o23.y} - prow[3];
+  const s2 p = smax(d0, splat(0)) + smax(d1, splat(0)) + smax(d2, splat(0)) + smax(d3, splat(0));
+  b.pos = i == 0 ? p : b.pos + p;
+  const s2 s0 = d0 + d1, s1 = d0 - d1, s2_ = d2 + d3, s3 = d2 - d3;
+  b.t[4 * i + 0] = s0 + s2_;
+  b.t[4 * i + 1] = s1 + s3;
+  b.t[4 * i + 2] = s0 - s2_;
+  b.t[4 * i + 3] = s1 - s3;
+}
+
+// Column butterflies, SATD and SAD of the block, added to the 32-bit accumulators.
+__device__ __forceinline__ void block_finish(const BlockAcc &b, uint32_t &sad0, uint32_t &sad1,
+                                             uint32_t &satd0, uint32_t &satd1) {
   s2 T = splat(0), dc = splat(0), ac = splat(0);
 #pragma unroll
   for (int c = 0; c < 4; c++) {
-    const s2 u0 = t[c] + t[4 + c], u1 = t[c] - t[4 + c];
-    const s2 u2_ = t[8 + c] + t[12 + c], u3 = t[8 + c] - t[12 + c];
+    const s2 u0 = b.t[c] + b.t[4 + c], u1 = b.t[c] - b.t[4 + c];
+    const s2 u2_ = b.t[8 + c] + b.t[12 + c], u3 = b.t[8 + c] - b.t[12 + c];
     if (c == 0) {
       dc = u0 + u2_;
       ac = u0 - u2_;
@@ -188,7 +191,7 @@ __device__ __forceinline__ void block_distortion(const s2 (&pred)[16], const uin
   const s2 adc = smax(dc, splat(0) - dc), aac = smax(ac, splat(0) - ac);
   const u2 U = as_u2(aac) + (as_u2(adc) >> (u2){2, 2});
   const u2 satd = as_u2(T) + ((U + (u2){1, 1}) >> (u2){1, 1});
-  const u2 sad = as_u2(pos + pos - dc);
+  const u2 sad = as_u2(b.pos + b.pos - dc);
   sad0 = __builtin_amdgcn_udot2(sad, (u2){1, 0}, sad0, false);
   sad1 = __builtin_amdgcn_udot2(sad, (u2){0, 1}, sad1, false);
   satd0 = __builtin_amdgcn_udot2(satd, (u2){1, 0}, satd0, false);
@@ -201,7 +204,7 @@ __device__ __forceinline__ uint2 lds_row4(const uint16_t *tile, int x, int y) {
 
 // Evaluate one WaveTask for a CU shape of size W x H.
 template <int W, int H>
-__device__ void run_task(const SearchArgs &a, const Tile &tile, int shape, int job0, int lane,
+__device__ __forceinline__ void run_task(const SearchArgs &a, const Tile &tile, int shape, int job0, int lane,
                          int ctu, int frame, int ctu_x, int ctu_y) {
   using G = Geo<W, H>;
   const mip_shape_desc sd = c_shapes[shape];
@@ -279,15 +282,16 @@ __device__ void run_task(const SearchArgs &a, const Tile &tile, int shape, int j
 
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
-    s2 pred[16];
+    BlockAcc acc;
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < 4; i++) {
+      s2 prow[4];
 #pragma unroll
-      for (int c = 0; c < 4; c++) pred[4 * i + c] = L.red(i, c);
-    uint2 orow[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) orow[i] = lds_row4(ot, cx, cy + i);
-    block_distortion(pred, orow, sad0, sad1, satd0, satd1);
+      for (int c = 0; c < 4; c++) prow[c] = L.red(i, c);
+      block_row(acc, i, prow, lds_row4(ot, cx, cy + i));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    block_finish(acc, sad0, sad1, satd0, satd1);
   } else {
     // ---- walk the strip downwards, 4x4 block by 4x4 block (intra.cl:815-1117)
     s2 prev[4], next[4];
@@ -298,17 +302,16 @@ __device__ void run_task(const SearchArgs &a, const Tile &tile, int shape, int j
       for (int c = 0; c < 4; c++) prev[c] = splat(fy > 0 ? t4[c] : padT);  // refT (vertical "before")
     }
     int kcur = -1;
+#pragma unroll 1
     for (int by = 0; by < H / 4; by++) {
-      s2 pred[16];
+      BlockAcc acc;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int y = 4 * by + i;
+        s2 prow[4];
         if constexpr (G::UV == 1) {
           const int leftv = fx > 0 ? rt[tidx(cx - 1, cy + y)] : padL;
-          s2 arow[4];
-          anchor_row<W, H>(L, y, x0, leftv, arow);
-#pragma unroll
-          for (int c = 0; c < 4; c++) pred[4 * i + c] = arow[c];
+          anchor_row<W, H>(L, y, x0, leftv, prow);
         } else {
           const int k = y >> G::LV;
           if (k != kcur) {  // wave-uniform
@@ -324,14 +327,13 @@ __device__ void run_task(const SearchArgs &a, const Tile &tile, int shape, int j
           const int o = (y & (G::UV - 1)) + 1;  // intra.cl:876-891
 #pragma unroll
           for (int c = 0; c < 4; c++)
-            pred[4 * i + c] = o == G::UV ? next[c]
-                                         : prev[c] + ((splat(o) * (next[c] - prev[c]) + splat(G::UV / 2)) >> splat(G::LV));
+            prow[c] = o == G::UV ? next[c]
+                                 : prev[c] + ((splat(o) * (next[c] - prev[c]) + splat(G::UV / 2)) >> splat(G::LV));
         }
+        block_row(acc, i, prow, lds_row4(ot, cx + x0, cy + y));
+        __builtin_amdgcn_sched_barrier(0);
       }
-      uint2 orow[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) orow[i] = lds_row4(ot, cx + x0, cy + 4 * by + i);
-      block_distortion(pred, orow, sad0, sad1, satd0, satd1);
+      block_finish(acc, sad0, sad1, satd0, satd1);
     }
   }
 
@@ -371,7 +373,7 @@ __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame,
 }
 
 template <bool ALT>
-__global__ __launch_bounds__(256) void mip_search_kernel(SearchArgs a) {
+__global__ __launch_bounds__(256, 3) void mip_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t *org = smem;
   uint16_t *ref = ALT ? smem + kTileElems : smem;
@@ -393,21 +395,15 @@ __global__ __launch_bounds__(256) void mip_search_kernel(SearchArgs a) {
   for (int t = slice * 4 + wave; t < a.ntasks; t += stride) {
     const WaveTask task = a.tasks[t];
     const int s = task.shape, j0 = task.job0;
-    switch (s) {
+    // Shapes share code by size class (17 distinct W x H among the 47 shapes).
+    switch (c_shape_class[s]) {
 #define MIP_CASE(idx, W, H) \
   case idx: run_task<W, H>(a, tile, s, j0, lane, ctu, frame, ctu_x, ctu_y); break;
       MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
       MIP_CASE(4, 32, 8) MIP_CASE(5, 8, 32) MIP_CASE(6, 16, 16) MIP_CASE(7, 16, 8)
-      MIP_CASE(8, 8, 16) MIP_CASE(9, 32, 16) MIP_CASE(10, 16, 32) MIP_CASE(11, 32, 8)
-      MIP_CASE(12, 32, 8) MIP_CASE(13, 8, 32) MIP_CASE(14, 8, 32) MIP_CASE(15, 16, 16)
-      MIP_CASE(16, 16, 16) MIP_CASE(17, 16, 16) MIP_CASE(18, 16, 8) MIP_CASE(19, 16, 8)
-      MIP_CASE(20, 16, 8) MIP_CASE(21, 16, 8) MIP_CASE(22, 16, 8) MIP_CASE(23, 8, 16)
-      MIP_CASE(24, 8, 16) MIP_CASE(25, 8, 16) MIP_CASE(26, 8, 16) MIP_CASE(27, 8, 16)
-      MIP_CASE(28, 32, 4) MIP_CASE(29, 4, 32) MIP_CASE(30, 16, 4) MIP_CASE(31, 4, 16)
-      MIP_CASE(32, 8, 8) MIP_CASE(33, 8, 4) MIP_CASE(34, 8, 4) MIP_CASE(35, 4, 8)
-      MIP_CASE(36, 4, 8) MIP_CASE(37, 16, 4) MIP_CASE(38, 4, 16) MIP_CASE(39, 8, 8)
-      MIP_CASE(40, 8, 8) MIP_CASE(41, 8, 8) MIP_CASE(42, 8, 8) MIP_CASE(43, 8, 8)
-      MIP_CASE(44, 8, 4) MIP_CASE(45, 4, 8) MIP_CASE(46, 4, 4)
+      MIP_CASE(8, 8, 16) MIP_CASE(9, 32, 4) MIP_CASE(10, 4, 32) MIP_CASE(11, 16, 4)
+      MIP_CASE(12, 4, 16) MIP_CASE(13, 8, 8) MIP_CASE(14, 8, 4) MIP_CASE(15, 4, 8)
+      MIP_CASE(16, 4, 4)
 #undef MIP_CASE
       default: break;
     }

@@ -1,0 +1,223 @@
+"""mipgpu -- Python host side of the MI355X-native VVC MIP search engine.
+
+Thin ctypes binding of ``libmipgpu.so`` (C ABI in ``include/mipgpu.h``).  The product
+path is the HIP library only: if it is missing this module raises at import of
+:class:`MipEngine` -- there is no CPU fallback.
+
+Mirrors the reference's operator surface (main.cpp + main_aux_functions.h):
+  * filter names / KernelIdx of the reference whitelist (constants.h:25-34),
+  * the per-frame cost table in the reference layout (constants.h:1558-1631),
+  * the CSV cost log (``mipgpu.log.write_cost_log``, main_aux_functions.h:735-798).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import layout
+from .layout import COSTS_PER_CTU, CUS_PER_CTU, SHAPES, UNAVAILABLE, num_ctus
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("MIPGPU_LIB", os.path.join(PKG_DIR, "lib", "libmipgpu.so"))
+
+# Reference whitelist order (constants.h:25-34); index == mip_filter_type.
+FILTERS = (
+    "filterFrame_1d_int",
+    "filterFrame_1d_float",
+    "filterFrame_2d_int_quarterCtu",
+    "filterFrame_2d_float_quarterCtu",
+    "filterFrame_1d_int_5x5",
+    "filterFrame_1d_float_5x5",
+    "filterFrame_2d_int_5x5_quarterCtu",
+    "filterFrame_2d_float_5x5_quarterCtu",
+)
+FILTER_NONE = -1
+
+
+class MipError(RuntimeError):
+    pass
+
+
+def filter_index(name) -> int:
+    """Filter name (reference spelling) or index -> mip_filter_type; None -> FILTER_NONE."""
+    if name is None:
+        return FILTER_NONE
+    if isinstance(name, (int, np.integer)):
+        return int(name)
+    if name not in FILTERS:
+        raise MipError(f"Filter type {name} not supported")  # main.cpp:74-76
+    return FILTERS.index(name)
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("filter", ctypes.c_int), ("kernel_idx", ctypes.c_int), ("max_batch", ctypes.c_int),
+                ("want_sad_satd", ctypes.c_int), ("slices_per_ctu", ctypes.c_int)]
+
+
+_lib = None
+
+
+def library():
+    """Load libmipgpu.so (raises if it was not built: the HIP path is mandatory)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MipError(f"{LIB_PATH} not found -- build it with `make -C vvc-mip-gpu_amd` "
+                       "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ip, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    sig = {
+        "mip_opts_default": (None, [ctypes.POINTER(_Opts)]),
+        "mip_engine_create": (ip, [ip, ip, ip, ctypes.POINTER(_Opts), ctypes.POINTER(vp)]),
+        "mip_engine_destroy": (ip, [vp]),
+        "mip_num_ctus": (ip, [ip, ip]),
+        "mip_costs_per_frame": (i64, [ip, ip]),
+        "mip_cus_per_frame": (i64, [ip, ip]),
+        "mip_shape_name": (ctypes.c_char_p, [ip]),
+        "mip_shape_info": (ip, [ip] + [ctypes.POINTER(ip)] * 5),
+        "mip_cu_position": (ip, [ip, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]),
+        "mip_filter_frames": (ip, [vp, vp, ip, ip, ip, vp]),
+        "mip_search_frames": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp]),
+        "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
+        "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
+        "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
+        "mip_last_error": (ctypes.c_char_p, []),
+        "mip_abi_version": (ip, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise MipError(library().mip_last_error().decode())
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()  # torch tensor
+
+
+class MipEngine:
+    """One engine per GPU (mip_engine_create).  Not thread safe."""
+
+    def __init__(self, width: int, height: int, device: int = 0, filter=None, kernel_idx: int = 0,
+                 max_batch: int = 1, want_sad_satd: bool = False, slices_per_ctu: int = 0):
+        L = library()
+        self.width, self.height = int(width), int(height)
+        self.nctus = num_ctus(self.width, self.height)
+        self.filter = filter_index(filter)
+        self.kernel_idx = int(kernel_idx)
+        self.max_batch = int(max_batch)
+        self.want_sad_satd = bool(want_sad_satd)
+        o = _Opts(self.filter, self.kernel_idx, self.max_batch, int(self.want_sad_satd), int(slices_per_ctu))
+        h = ctypes.c_void_p()
+        _check(L.mip_engine_create(int(device), self.width, self.height, ctypes.byref(o), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            library().mip_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def costs_per_frame(self) -> int:
+        return self.nctus * COSTS_PER_CTU
+
+    @property
+    def cus_per_frame(self) -> int:
+        return self.nctus * CUS_PER_CTU
+
+    # ---------------------------------------------------------------- host API
+    def _frames(self, frames):
+        f = np.ascontiguousarray(frames, dtype=np.uint16)
+        if f.ndim == 2:
+            f = f[None]
+        if f.shape[1:] != (self.height, self.width):
+            raise MipError(f"frames of shape {f.shape[1:]} do not match {self.height}x{self.width}")
+        return f
+
+    def search(self, frames, refs=None, costs=True, best=False, sad_satd=False):
+        """Full MIP search of host frames ([F,H,W] or [H,W] uint16).  Returns a dict with
+        'cost' [F, nCTUs*97840] int32 and optionally 'best_mode' / 'best_cost' [F, nCTUs*5380],
+        'sad' / 'satd'."""
+        f = self._frames(frames)
+        r = None if refs is None else self._frames(refs)
+        n = f.shape[0]
+        out = {}
+        cost = np.empty((n, self.costs_per_frame), np.int32) if costs else None
+        bm = np.empty((n, self.cus_per_frame), np.uint8) if best else None
+        bc = np.empty((n, self.cus_per_frame), np.int32) if best else None
+        sad = np.empty((n, self.costs_per_frame), np.int32) if sad_satd else None
+        satd = np.empty((n, self.costs_per_frame), np.int32) if sad_satd else None
+        _check(library().mip_search_frames(self._h, _ptr(f), _ptr(r), n, _ptr(cost), _ptr(bm), _ptr(bc),
+                                           _ptr(sad), _ptr(satd)))
+        for k, v in (("cost", cost), ("best_mode", bm), ("best_cost", bc), ("sad", sad), ("satd", satd)):
+            if v is not None:
+                out[k] = v
+        return out
+
+    def filter_frames(self, frames, filter, kernel_idx=0):
+        f = self._frames(frames)
+        out = np.empty_like(f)
+        _check(library().mip_filter_frames(self._h, _ptr(f), f.shape[0], filter_index(filter), int(kernel_idx),
+                                           _ptr(out)))
+        return out
+
+    # -------------------------------------------------------------- device API
+    def search_device(self, frames, refs=None, costs=None, sad=None, satd=None, best_mode=None,
+                      best_cost=None, stream=None):
+        """Asynchronous search on device tensors (torch, int16/uint16 [F,H,W]) on `stream`
+        (a torch.cuda.Stream; default: torch's current stream)."""
+        import torch
+        n = frames.shape[0]
+        if costs is None:
+            costs = torch.empty((n, self.costs_per_frame), dtype=torch.int32, device=frames.device)
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        _check(library().mip_search_device(self._h, _ptr(frames), _ptr(refs), n, _ptr(costs), _ptr(sad),
+                                           _ptr(satd), _ptr(best_mode), _ptr(best_cost),
+                                           ctypes.c_void_p(s.cuda_stream)))
+        return costs
+
+    def time_search_device(self, frames, costs, refs=None, reps=10) -> float:
+        ms = library().mip_time_search_device(self._h, _ptr(frames), _ptr(refs), frames.shape[0], _ptr(costs),
+                                              int(reps))
+        if ms < 0:
+            raise MipError(library().mip_last_error().decode())
+        return ms
+
+
+def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
+    import torch
+    n, h, w = frames_in.shape
+    s = stream if stream is not None else torch.cuda.current_stream(frames_in.device)
+    _check(library().mip_filter_device(_ptr(frames_in), _ptr(frames_out), w, h, n, filter_index(filter),
+                                       int(kernel_idx), ctypes.c_void_p(s.cuda_stream)))
+    return frames_out
+
+
+__all__ = ["MipEngine", "MipError", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "library",
+           "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]
