@@ -107,7 +107,9 @@ def reference_gpu(width, height, frames, seed):
                               "--height", str(height), "--frames", str(frames), "--synth", "0:%x" % seed,
                               "--reps", "2"], capture_output=True, timeout=180, check=True).stdout.decode()
         d = json.loads(out.strip().splitlines()[-1])
-        return {"value": round(1000.0 / d["device_ms_per_frame"], 2), "unit": "frames/s (device time)",
+        if not d["device_ms_per_frame"] > 0:
+            return {"error": "no device timing", "raw": d}
+        return {"value": round(1000.0 / d["device_ms_per_frame"], 3), "unit": "frames/s (device time)",
                 "wall_value": round(1000.0 / d["wall_ms_per_frame"], 2),
                 "kernel_ms_per_frame": d["kernel_ms"], "device": d["device"],
                 "note": "reference intra.cl kernels (initBoundaries, MIP_ReducedPred, 3x upsampleDistortion) "
@@ -149,7 +151,7 @@ def main():
     frames = torch.from_numpy(host.astype(np.int16)).to(dev)
     eng = MipEngine(W, H, device=local_rank, max_batch=B, slices_per_ctu=args.slices)
     costs = torch.empty((B, eng.costs_per_frame), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # the search kernels and the timing events share it
 
     for _ in range(args.warmup):
         eng.search_device(frames, costs=costs, stream=stream)
@@ -207,7 +209,7 @@ def main():
                 ref = reference_gpu(W, H, min(B, 4), args.seed)
                 if ref is not None:
                     res["reference_gpu"] = ref
-                    if "value" in ref:
+                    if ref.get("value"):
                         res["speedup_vs_reference_gpu"] = round(value / ref["value"], 2)
         print(json.dumps(res), flush=True)
     eng.close()

@@ -97,7 +97,8 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
                       int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out);
 
 /* Device-resident variant (inputs already in HBM; all pointers are device pointers,
- * `stream` is a hipStream_t or NULL for the engine stream).  Asynchronous on `stream`.
+ * `stream` is a hipStream_t; NULL means the default (null) stream, as in HIP).
+ * Asynchronous on `stream`.
  * d_refs NULL: originals, or the engine filter applied into engine scratch.
  * d_costs required; the optional outputs may be NULL. */
 int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
@@ -109,8 +110,8 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
                       int nframes, int filter, int kernel_idx, void *stream);
 
 /* Kernel-only timing of the search on resident buffers: runs `reps` launches of the
- * fused search for `nframes` device frames, returns the mean device time per launch in
- * milliseconds (HIP events on the engine stream), or <0. */
+ * fused search for `nframes` device frames on the engine's own stream, returns the mean
+ * device time per launch in milliseconds (HIP events on that stream), or <0. */
 double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
                               int nframes, int32_t *d_costs, int reps);
 

@@ -82,10 +82,17 @@ static cl_program load_program(cl_context ctx, cl_device_id dev, const char *dir
   return p;
 }
 
-static double ev_ms(cl_event e) {
+/* Device time of a finished command from its profiling timestamps; falls back to the
+ * host wall time around enqueue+clFinish (passed in) when the timestamps are unusable. */
+static int g_event_fallbacks = 0;
+static double ev_ms(cl_event e, double wall_ms) {
   cl_ulong a = 0, b = 0;
-  clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_START, sizeof a, &a, NULL);
-  clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_END, sizeof b, &b, NULL);
+  cl_int e1 = clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_START, sizeof a, &a, NULL);
+  cl_int e2 = clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_END, sizeof b, &b, NULL);
+  if (e1 != CL_SUCCESS || e2 != CL_SUCCESS || b < a || (double)(b - a) * 1e-6 > 1e3 * wall_ms + 1e3) {
+    g_event_fallbacks++;
+    return wall_ms;
+  }
   return (double)(b - a) * 1e-6;
 }
 
@@ -202,9 +209,10 @@ int main(int argc, char **argv) {
         clSetKernelArg(k_filt, 4, sizeof(cl_int), &kidx);
         clSetKernelArg(k_filt, 5, sizeof(cl_int), &rep);
         size_t l = 256, g = (size_t)nctus * 4 * 256;
+        double w0 = now_s();
         CHECK(clEnqueueNDRangeKernel(q, k_filt, 1, NULL, &g, &l, 0, NULL, &e), "filter");
         CHECK(clFinish(q), "finish filter");
-        t_filt += ev_ms(e);
+        t_filt += ev_ms(e, (now_s() - w0) * 1e3);
         clReleaseEvent(e);
         if (filtered)
           CHECK(clEnqueueReadBuffer(q, m_filt, CL_TRUE, rep * fs * 2, fs * 2, filtered + fs * f, 0, NULL, NULL), "D2H filt");
@@ -219,9 +227,10 @@ int main(int argc, char **argv) {
       clSetKernelArg(k_init, 6, sizeof(cl_mem), &m_refL);
       clSetKernelArg(k_init, 7, sizeof(cl_int), &rep);
       size_t l = 128, g = (size_t)nctus * 47 * 128;
+      double w0 = now_s();
       CHECK(clEnqueueNDRangeKernel(q, k_init, 1, NULL, &g, &l, 0, NULL, &e), "initBoundaries");
       CHECK(clFinish(q), "finish init");
-      t_init += ev_ms(e);
+      t_init += ev_ms(e, (now_s() - w0) * 1e3);
       clReleaseEvent(e);
 
       clSetKernelArg(k_red, 0, sizeof(cl_mem), &m_pred);
@@ -233,9 +242,10 @@ int main(int argc, char **argv) {
       clSetKernelArg(k_red, 6, sizeof(cl_int), &rep);
       l = 256;
       g = (size_t)nctus * 47 * 256;
+      w0 = now_s();
       CHECK(clEnqueueNDRangeKernel(q, k_red, 1, NULL, &g, &l, 0, NULL, &e), "MIP_ReducedPred");
       CHECK(clFinish(q), "finish reduced");
-      t_red += ev_ms(e);
+      t_red += ev_ms(e, (now_s() - w0) * 1e3);
       clReleaseEvent(e);
 
       for (int s = 0; s < 3; s++) {
@@ -254,9 +264,10 @@ int main(int argc, char **argv) {
         clSetKernelArg(k, a++, sizeof(cl_mem), &m_refL);
         clSetKernelArg(k, a++, sizeof(cl_int), &rep);
         g = (size_t)up_wgs[s] * 256;
+        w0 = now_s();
         CHECK(clEnqueueNDRangeKernel(q, k, 1, NULL, &g, &l, 0, NULL, &e), "upsampleDistortion");
         CHECK(clFinish(q), "finish upsample");
-        t_up[s] += ev_ms(e);
+        t_up[s] += ev_ms(e, (now_s() - w0) * 1e3);
         clReleaseEvent(e);
       }
       const size_t off = (size_t)rep * nctus * COST_PER_CTU * 8, cnt = (size_t)nctus * COST_PER_CTU;
@@ -284,8 +295,9 @@ int main(int argc, char **argv) {
   printf("{\"device\": \"%s\", \"width\": %d, \"height\": %d, \"frames\": %d, \"filter\": \"%s\", "
          "\"kernel_ms\": {\"filter\": %.4f, \"initBoundaries\": %.4f, \"MIP_ReducedPred\": %.4f, "
          "\"upsampleDistortion_s2\": %.4f, \"upsampleDistortion_s1\": %.4f, \"upsampleDistortion_s0\": %.4f}, "
-         "\"device_ms_per_frame\": %.4f, \"wall_ms_per_frame\": %.4f}\n",
+         "\"device_ms_per_frame\": %.4f, \"wall_ms_per_frame\": %.4f, \"event_fallbacks\": %d}\n",
          dname, W, H, frames, filter ? filter : "", t_filt / frames, t_init / frames, t_red / frames,
-         t_up[0] / frames, t_up[1] / frames, t_up[2] / frames, dev_ms / frames, wall * 1e3 / frames);
+         t_up[0] / frames, t_up[1] / frames, t_up[2] / frames, dev_ms / frames, wall * 1e3 / frames,
+         g_event_fallbacks);
   return 0;
 }

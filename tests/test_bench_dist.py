@@ -1,0 +1,54 @@
+"""Multi-process plumbing of bench.py on CPU (gloo, world_size 2): frame sharding and the
+max-over-ranks timing reduction used with RCCL on the GPU box."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r, lr, w = bench.dist_env()
+    elapsed = 1.0 + rank  # rank 1 is the slow one
+    m = bench.dist_max(elapsed, w)
+    seeds = [None] * w
+    dist.all_gather_object(seeds, bench.shard_seed(0x1080, r))
+    q.put((r, lr, w, m, seeds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_max_and_sharding():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r, (rank, lr, w, m, seeds) in enumerate(res):
+        assert (rank, lr, w) == (r, r, 2)
+        assert m == 2.0                       # max over ranks
+        assert len(set(seeds)) == 2           # disjoint frame shards
+
+
+def test_aggregate_is_whole_job_throughput():
+    v, ms = bench.aggregate(frames_per_step=8, steps=10, world=4, max_elapsed_s=2.0)
+    assert v == 8 * 10 * 4 / 2.0 and ms == 200.0
+    assert bench.algorithmic_bytes_per_frame(1920, 1080) == 1920 * 1080 * 2 + 135 * 97840 * 4

@@ -261,7 +261,7 @@ int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d
   if (!e) return fail("engine is NULL");
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, d_best_mode, d_best_cost,
-                            stream ? (hipStream_t)stream : e->stream);
+                            (hipStream_t)stream);
 }
 
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
