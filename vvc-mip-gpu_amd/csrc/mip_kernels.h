@@ -7,7 +7,7 @@
 namespace mipgpu {
 
 // One wave-sized piece of work: 64 lanes of (CU, mode pair, 4-column strip) of one
-// CU shape, starting at job index `job0` (job = cu * modes + pair).
+// CU shape, starting at job index `job0` (job = pair * ncu + cu).
 struct WaveTask {
   uint16_t shape;
   uint16_t job0;

@@ -214,7 +214,9 @@ __device__ __forceinline__ void run_task(const SearchArgs &a, const Tile &tile, 
   const int sx = lane % G::S, x0 = 4 * sx;
   const bool active = job < njobs;
   if (!active) job = njobs - 1;
-  const int cu = job / modes, q = job - cu * modes;
+  // q-major job order (job = q * ncu + cu): the lanes of a wave share the mode pair, so the
+  // weight-row reads of the matrix products broadcast instead of bank-conflicting.
+  const int q = job / sd.ncu, cu = job - q * sd.ncu;
   const int cx = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols);
   const int cy = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
   const int fx = ctu_x + cx, fy = ctu_y + cy;

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -62,9 +63,24 @@ std::vector<int16_t> expand_weights() {
 // Per-CTU wave-task list: shapes ordered by lane cost (rows per strip, descending) so the
 // round-robin assignment of tasks to waves balances; tasks of one shape stay adjacent so
 // co-resident waves run the same code.
+// MIPGPU_SHAPE_FILTER="i,j,..." (profiling knob) restricts the search to those shapes.
 std::vector<mipgpu::WaveTask> build_tasks() {
-  std::vector<int> order(MIP_NUM_SHAPES);
-  for (int i = 0; i < MIP_NUM_SHAPES; i++) order[i] = i;
+  std::vector<int> order;
+  const char *flt = getenv("MIPGPU_SHAPE_FILTER");
+  for (int i = 0; i < MIP_NUM_SHAPES; i++) {
+    if (flt && *flt) {
+      bool keep = false;
+      for (const char *p = flt; *p;) {
+        char *end;
+        const long v = strtol(p, &end, 10);
+        if (end == p) break;
+        keep |= v == i;
+        p = *end ? end + 1 : end;
+      }
+      if (!keep) continue;
+    }
+    order.push_back(i);
+  }
   std::stable_sort(order.begin(), order.end(), [](int a, int b) { return kShapes[a].h > kShapes[b].h; });
   std::vector<mipgpu::WaveTask> t;
   for (int s : order) {
