@@ -6,11 +6,19 @@
 
 namespace mipgpu {
 
-// One wave-sized piece of work: 64 lanes of (CU, mode pair, 4-column strip) of one
-// CU shape, starting at job index `job0` (job = pair * ncu + cu).
+// Work is organised per 64x64 quadrant of a CTU (no CU of the 47 shapes straddles a
+// quadrant).  A *job* is one (CU, mode pair) of a shape inside the quadrant; a *wave task*
+// is up to 64/S jobs of one shape (S = W/4 strips per CU), one lane per (job, strip).
+struct Job {
+  uint16_t cu;    // CU index within its shape (reference order, constants.h:1235-1354)
+  uint8_t pair;   // mode pair q: modes 2q, 2q+1 (transposed when 2q >= modes)
+  uint8_t pad;
+};
 struct WaveTask {
-  uint16_t shape;
-  uint16_t job0;
+  uint8_t shape;
+  uint8_t njobs;
+  uint16_t pad;
+  uint32_t job0;  // index into the quadrant's job array
 };
 
 struct SearchArgs {
@@ -19,12 +27,13 @@ struct SearchArgs {
   int32_t *cost;          // [frames][nctus][97840]  min(2*SAD, SATD)
   int32_t *sad;           // optional, same layout
   int32_t *satd;          // optional, same layout
-  const WaveTask *tasks;  // per-CTU wave-task list (heaviest first)
+  const WaveTask *tasks;  // 4 per-quadrant task lists, concatenated (heaviest first)
+  const Job *jobs;        // 4 per-quadrant job arrays, concatenated
   const int16_t *weights; // expanded MIP weights, see kWeightWords
   int width, height;
   int ctu_cols, nctus;
-  int ntasks;
-  int slices;             // workgroups per CTU
+  int task_begin[5];      // quadrant q's tasks: [task_begin[q], task_begin[q+1])
+  int slices;             // workgroups per CTU quadrant
 };
 
 // Expanded weight table (int16): 16-byte rows of 8 taps, index (mode*outputs + j)*8.

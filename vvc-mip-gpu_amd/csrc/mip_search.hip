@@ -2,25 +2,30 @@
 //
 // One kernel does what the reference splits over initBoundaries, MIP_ReducedPred and
 // three upsampleDistortion builds (intra.cl:17-1171): boundary downsampling, the MIP
-// matrix-vector products, linear upsampling, SAD and 4x4-Hadamard SATD, and the
-// min(2*SAD, SATD) cost, without writing any intermediate to HBM (the reference
-// round-trips ~1.2 GB of reduced predictions per 1080p frame, main.cpp:443-444).
+// matrix-vector products, linear upsampling, SAD and 4x4-Hadamard SATD and the
+// min(2*SAD, SATD) cost -- without any intermediate in HBM (the reference round-trips
+// ~1.2 GB of reduced predictions per 1080p frame, main.cpp:443-444).
 //
 // Work decomposition
-//   workgroup = (CTU, slice), 256 threads.  The CTU's samples (+1 row above, +4 columns
-//   left) are staged once in LDS; so are the expanded MIP weights.
-//   wave      = one WaveTask: 64 lanes of a single CU shape (so every loop bound and
-//               branch is wave-uniform).
-//   lane      = (CU, mode pair, 4-column strip).  The two modes of a pair travel in the
-//               two 16-bit halves of every VGPR, so upsampling, SAD and the Hadamard run
-//               as packed int16 VALU ops (v_pk_*) - all intermediates provably fit in
-//               16 bits (see the bounds noted at each step).
-//   The strip lanes of one (CU, pair) are adjacent; their partial SAD/SATD are reduced
-//   with cross-lane shuffles at the end.
+//   workgroup = (CTU quadrant, slice), kWaves waves.  No CU of the 47 shapes straddles a
+//               64x64 quadrant, so a workgroup stages only its quadrant (+1 row above,
+//               +4 columns left: the reference samples) in LDS, 8.8 KB.
+//   wave      = one WaveTask: up to 64/S jobs (CU, mode pair) of ONE shape, so every
+//               loop bound and branch is wave-uniform.
+//   lane      = (job, 4-column strip).  The two modes of a pair travel in the two 16-bit
+//               halves of each VGPR: upsampling, SAD and the Hadamard are packed int16
+//               VALU ops (v_pk_*); all intermediates provably fit 16 bits (bounds inline).
+//   Phase A   (shapes whose strips share reduced-prediction values, W > R): the wave
+//               computes each job's reduced prediction once (v_dot2_i32_i16) into a
+//               wave-private LDS scratch in the reference's stored order.
+//   Phase B   every lane walks its strip 4x4 block by 4x4 block: anchors (horizontal
+//               pass), vertical interpolation, SAD and SATD; strips of one job are adjacent
+//               lanes and are combined with xor shuffles.  Shapes with W == R (no sharing)
+//               compute their matrix products directly in phase B.
 //
-// Bit-exactness: every arithmetic step restates the reference integer semantics
-// (citations inline); tests/test_gpu_parity.py checks the tables bit for bit against the
-// C oracle, which is itself pinned to the reference kernels' outputs (tests/golden/).
+// Bit-exactness: every step restates the reference integer semantics (citations inline);
+// tests/test_gpu_parity.py checks the tables bit for bit against the C oracle, which is
+// pinned to the reference kernels' own outputs (tests/golden/).
 #include "mip_kernels.h"
 #include "mip_tables.h"
 
@@ -31,7 +36,7 @@ typedef short __attribute__((ext_vector_type(2))) s2;
 typedef unsigned short __attribute__((ext_vector_type(2))) u2;
 
 __constant__ mip_shape_desc c_shapes[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;
-// Size class of each shape (index into the run_task<W, H> instantiations below).
+// Size class of each shape (index into the run_task<W, H> instantiations).
 __constant__ uint8_t c_shape_class[MIP_NUM_SHAPES] = {
     0, 1, 2, 3, 4, 5, 6, 7, 8,                                  // aligned SizeId 2
     2, 3, 4, 4, 5, 5, 6, 6, 6, 7, 7, 7, 7, 7, 8, 8, 8, 8, 8,    // NA SizeId 2
@@ -39,14 +44,19 @@ __constant__ uint8_t c_shape_class[MIP_NUM_SHAPES] = {
     11, 12, 13, 13, 13, 13, 13, 14, 15,                         // NA SizeId 1
     16};                                                        // 4x4
 
-constexpr int kPitch = 132;   // LDS row pitch in samples: 66 dwords, rows rotate banks by 2
-constexpr int kColOff = 4;    // LDS column of CTU column 0 (columns -4..-1 hold the left halo)
-constexpr int kTileElems = (129 * kPitch + 7) / 8 * 8;  // CTU rows -1..127, 16-B multiple
+constexpr int kWaves = 8;        // waves per workgroup
+constexpr int kPitch = 68;       // LDS row pitch in samples (34 dwords: conflict-free rows)
+constexpr int kColOff = 4;       // LDS column of quadrant column 0 (-4..-1: left halo)
+constexpr int kTileElems = (65 * kPitch + 7) / 8 * 8;  // quadrant rows -1..63
+constexpr int kJobWords = 8;     // job-table entry (dwords)
+constexpr int kScratchWords = 16 * 65;                  // 16 jobs x (64 + 1) packed pairs
+constexpr int kWaveWords = 64 * kJobWords + kScratchWords;
 constexpr int kUnavailable = 0x7fffffff;
 
 __device__ __forceinline__ int tidx(int x, int y) { return (y + 1) * kPitch + x + kColOff; }
 __device__ __forceinline__ s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
 __device__ __forceinline__ u2 as_u2(s2 v) { return __builtin_bit_cast(u2, v); }
+__device__ __forceinline__ uint32_t as_u32(s2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ s2 splat(int v) { return s2{(short)v, (short)v}; }
 __device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ s2 smin(s2 a, s2 b) { return __builtin_elementwise_min(a, b); }
@@ -55,6 +65,13 @@ constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
 
 __device__ __forceinline__ int axis_pos(int base, int step, int dual, int i) {
   return dual ? base + (i >> 1) * step + (i & 1) * dual : base + i * step;
+}
+
+// LDS fence for data handed between lanes of ONE wave (wave-private scratch).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Compile-time geometry of a CU shape (W x H).
@@ -67,13 +84,8 @@ struct Geo {
   static constexpr int UH = W / R, UV = H / R;        // upsampling factors
   static constexpr int LH = ilog2c(UH), LV = ilog2c(UV);
   static constexpr int S = W / 4;                     // strips per CU
+  static constexpr bool DIRECT = UH == 1;             // no reduced value shared by strips
   static constexpr int WROW = SID == 2 ? 0 : (SID == 1 ? kWeightRowOffS1 : kWeightRowOffS0);
-};
-
-struct Tile {
-  const uint16_t *org;  // distortion samples
-  const uint16_t *ref;  // reference samples (== org unless alternative references)
-  const int16_t *w;     // expanded weights
 };
 
 // Matrix-vector product of one mode for output j, intra.cl:449-482: ((offset + p.w) >> 6)
@@ -92,67 +104,109 @@ __device__ __forceinline__ int gemv(const s2 (&p)[4], const int16_t *wrow, int o
     acc = __builtin_amdgcn_sdot2(p[2], as_s2(w.z), acc, false);
     acc = __builtin_amdgcn_sdot2(p[3], as_s2(w.w), acc, false);
   }
-  const int v = (acc >> 6) + b0;
-  return min(max(v, 0), 1023);
+  return min(max((acc >> 6) + b0, 0), 1023);
 }
 
-// Per-lane state of one (CU, mode pair, strip) evaluation.
-template <int W, int H>
-struct Lane {
-  using G = Geo<W, H>;
+// MIP inputs of one job: packed p vector, offset, b0, weight rows of its two modes.
+struct MipIn {
   s2 p[4];
   int offset, b0;
-  const int16_t *w0, *w1;  // weight rows of the two modes
+  int wrow;        // first weight row (16-B rows) of mode 2q mod modes
   bool transposed;
-
-  // Reduced-prediction value of both modes at stored position (k, kx); transposed modes
-  // store output j at (j % R, j / R), intra.cl:402-406, 485.
-  __device__ __forceinline__ s2 red(int k, int kx) const {
-    const int j = transposed ? kx * G::R + k : k * G::R + kx;
-    const int a = gemv<G::SID>(p, w0 + j * 8, offset, b0);
-    const int b = gemv<G::SID>(p, w1 + j * 8, offset, b0);
-    return s2{(short)a, (short)b};
-  }
 };
 
-// Horizontally upsampled anchor row k (CU row k*UV + UV-1) at the 4 strip columns
-// x0..x0+3, intra.cl:816-843: the first UH columns interpolate from the left boundary.
-// Values stay in [0, 1023]; (UH-o)*before + o*after + UH/2 <= 8188 fits int16.
-template <int W, int H>
-__device__ __forceinline__ void anchor_row(const Lane<W, H> &L, int k, int x0, int left_k, s2 (&a)[4]) {
-  using G = Geo<W, H>;
-  if constexpr (G::UH == 1) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) a[c] = L.red(k, x0 + c);
-  } else if constexpr (G::UH == 2) {
-    const int kx = x0 >> 1;  // covers kx, kx+1
-    const s2 r0 = L.red(k, kx), r1 = L.red(k, kx + 1);
-    const s2 before = kx == 0 ? splat(left_k) : L.red(k, max(kx - 1, 0));
-    a[0] = (before + r0 + splat(1)) >> splat(1);
-    a[1] = r0;
-    a[2] = (r0 + r1 + splat(1)) >> splat(1);
-    a[3] = r1;
-  } else {
-    const int kx = x0 >> G::LH;
-    const s2 after = L.red(k, kx);
-    const s2 before = kx == 0 ? splat(left_k) : L.red(k, max(kx - 1, 0));
-    const s2 delta = after - before;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int o = ((x0 + c) & (G::UH - 1)) + 1;
-      a[c] = before + ((splat(o) * delta + splat(G::UH / 2)) >> splat(G::LH));
-    }
-  }
+// Per-CU geometry + boundary padding, quadrant-relative.
+struct CuPos {
+  int lx, ly;      // CU origin inside the quadrant
+  bool top, left;  // reference row above / column left lies inside the frame
+  int padT, padL;  // padding values, intra.cl:102-106, 238-242
+};
+
+__device__ __forceinline__ CuPos cu_pos(const mip_shape_desc &sd, int cu, int ctu_x, int ctu_y, int qx, int qy,
+                                        const uint16_t *rt);
+
+__device__ __forceinline__ uint2 lds_row4(const uint16_t *tile, int x, int y) {
+  return *reinterpret_cast<const uint2 *>(tile + tidx(x, y));
 }
 
-// SAD and SATD of one 4x4 block for both modes (packed), added to 32-bit accumulators.
-// d = orig - pred in [-1023, 1023].  Hadamard intermediates: rows <= 4092, column sums
-// <= 8184, DC <= 16368 -- all int16.  SATD per block (kernel_aux_functions.cl:142-249):
-//   (sum_k |c_k| - |c_0| + (|c_0| >> 2) + 1) >> 1.
-// The last butterfly is folded with |a+b| + |a-b| = 2 max(|a|, |b|), so with T = sum of
-// the seven non-DC pair maxima and U = |AC0| + (|DC| >> 2):  satd = T + ((U + 1) >> 1).
-// By Parseval (||c||_2 = 4 ||d||_2) satd <= 32736 and T <= satd, so u16 holds both.
-// SAD = sum |d| = 2 * sum max(d, 0) - DC, exact in 16 bits for the same reason.
+__device__ __forceinline__ CuPos cu_pos(const mip_shape_desc &sd, int cu, int ctu_x, int ctu_y, int qx, int qy,
+                                        const uint16_t *rt) {
+  CuPos c;
+  const int cx = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols);
+  const int cy = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
+  c.lx = cx - qx;
+  c.ly = cy - qy;
+  c.top = ctu_y + cy > 0;
+  c.left = ctu_x + cx > 0;
+  c.padT = c.left ? rt[tidx(c.lx - 1, c.ly)] : 512;   // top edge: sample (x-1, 0)
+  c.padL = c.top ? rt[tidx(c.lx, c.ly - 1)] : 512;    // left edge: sample (0, y-1)
+  return c;
+}
+
+// Reduced boundaries and MIP input vector of one job, intra.cl:71-73, 127-141, 202-204,
+// 259-279 (box downsampling; a factor of 1 is a copy) and intra.cl:415-454.
+template <int W, int H>
+__device__ __forceinline__ MipIn mip_inputs(const CuPos &c, int pair, int modes, const uint16_t *rt) {
+  using G = Geo<W, H>;
+  constexpr int dfT = W / G::RBS, l2T = ilog2c(dfT), rndT = dfT > 1 ? dfT / 2 : 0;
+  constexpr int dfL = H / G::RBS, l2L = ilog2c(dfL), rndL = dfL > 1 ? dfL / 2 : 0;
+  int redT[G::RBS], redL[G::RBS];
+#pragma unroll
+  for (int i = 0; i < G::RBS; i++) {
+    int s = 0;
+    if constexpr (dfT >= 4) {
+#pragma unroll
+      for (int t = 0; t < dfT; t += 4) {
+        const uint2 v = lds_row4(rt, c.lx + i * dfT + t, c.ly - 1);
+        s += (v.x & 0xffff) + (v.x >> 16) + (v.y & 0xffff) + (v.y >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < dfT; t++) s += rt[tidx(c.lx + i * dfT + t, c.ly - 1)];
+    }
+    redT[i] = c.top ? (s + rndT) >> l2T : c.padT;
+    int l = 0;
+#pragma unroll
+    for (int t = 0; t < dfL; t++) l += rt[tidx(c.lx - 1, c.ly + i * dfL + t)];
+    redL[i] = c.left ? (l + rndL) >> l2L : c.padL;
+  }
+  MipIn m;
+  const int m0 = 2 * pair;
+  m.transposed = m0 >= modes;
+  const int mw = m.transposed ? m0 - modes : m0;
+  int b[8];
+#pragma unroll
+  for (int i = 0; i < G::RBS; i++) {
+    b[i] = m.transposed ? redL[i] : redT[i];
+    b[G::RBS + i] = m.transposed ? redT[i] : redL[i];
+  }
+#pragma unroll
+  for (int i = 2 * G::RBS; i < 8; i++) b[i] = b[0];
+  m.b0 = b[0];
+  int pv[8], psum = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) pv[i] = b[i] - m.b0;
+  pv[0] = G::SID == 2 ? 0 : 512 - m.b0;  // intra.cl:446
+#pragma unroll
+  for (int i = 0; i < 2 * G::RBS; i++) psum += pv[i];
+  m.offset = 32 - 32 * psum;             // intra.cl:449-454
+#pragma unroll
+  for (int i = 0; i < 4; i++) m.p[i] = s2{(short)pv[2 * i], (short)pv[2 * i + 1]};
+  m.wrow = G::WROW + mw * G::NOUT;
+  return m;
+}
+
+// Both modes of a pair at stored reduced position (k, kx); transposed modes store output
+// j at (j % R, j / R), intra.cl:402-406, 485.
+template <int W, int H>
+__device__ __forceinline__ s2 red_direct(const MipIn &m, const int16_t *w, int k, int kx) {
+  using G = Geo<W, H>;
+  const int j = m.transposed ? kx * G::R + k : k * G::R + kx;
+  const int a = gemv<G::SID>(m.p, w + (m.wrow + j) * 8, m.offset, m.b0);
+  const int b = gemv<G::SID>(m.p, w + (m.wrow + G::NOUT + j) * 8, m.offset, m.b0);
+  return s2{(short)a, (short)b};
+}
+
 struct BlockAcc {
   s2 t[16];  // row-transformed residual
   s2 pos;    // sum of max(d, 0)
@@ -172,9 +226,15 @@ __device__ __forceinline__ void block_row(BlockAcc &b, int i, const s2 (&prow)[4
   b.t[4 * i + 3] = s1 - s3;
 }
 
-// Column butterflies, SATD and SAD of the block, added to the 32-bit accumulators.
-__device__ __forceinline__ void block_finish(const BlockAcc &b, uint32_t &sad0, uint32_t &sad1,
-                                             uint32_t &satd0, uint32_t &satd1) {
+// SAD and SATD of the block for both modes (packed 16-bit).
+// d = orig - pred in [-1023, 1023].  Hadamard intermediates: rows <= 4092, column sums
+// <= 8184, DC <= 16368 -- all int16.  SATD per block (kernel_aux_functions.cl:142-249):
+//   (sum_k |c_k| - |c_0| + (|c_0| >> 2) + 1) >> 1.
+// The last butterfly is folded with |a+b| + |a-b| = 2 max(|a|, |b|), so with T = sum of
+// the seven non-DC pair maxima and U = |AC0| + (|DC| >> 2):  satd = T + ((U + 1) >> 1).
+// By Parseval (||c||_2 = 4 ||d||_2) satd <= 32736 and T <= satd, so u16 holds both.
+// SAD = sum |d| = 2 * sum max(d, 0) - DC <= 16368, exact in 16 bits for the same reason.
+__device__ __forceinline__ void block_finish(const BlockAcc &b, u2 &sad, u2 &satd) {
   s2 T = splat(0), dc = splat(0), ac = splat(0);
 #pragma unroll
   for (int c = 0; c < 4; c++) {
@@ -190,183 +250,217 @@ __device__ __forceinline__ void block_finish(const BlockAcc &b, uint32_t &sad0, 
   }
   const s2 adc = smax(dc, splat(0) - dc), aac = smax(ac, splat(0) - ac);
   const u2 U = as_u2(aac) + (as_u2(adc) >> (u2){2, 2});
-  const u2 satd = as_u2(T) + ((U + (u2){1, 1}) >> (u2){1, 1});
-  const u2 sad = as_u2(b.pos + b.pos - dc);
-  sad0 = __builtin_amdgcn_udot2(sad, (u2){1, 0}, sad0, false);
-  sad1 = __builtin_amdgcn_udot2(sad, (u2){0, 1}, sad1, false);
-  satd0 = __builtin_amdgcn_udot2(satd, (u2){1, 0}, satd0, false);
-  satd1 = __builtin_amdgcn_udot2(satd, (u2){0, 1}, satd1, false);
+  satd = as_u2(T) + ((U + (u2){1, 1}) >> (u2){1, 1});
+  sad = as_u2(b.pos + b.pos - dc);
 }
 
-__device__ __forceinline__ uint2 lds_row4(const uint16_t *tile, int x, int y) {
-  return *reinterpret_cast<const uint2 *>(tile + tidx(x, y));
-}
-
-// Evaluate one WaveTask for a CU shape of size W x H.
-template <int W, int H>
-__device__ __forceinline__ void run_task(const SearchArgs &a, const Tile &tile, int shape, int job0, int lane,
-                         int ctu, int frame, int ctu_x, int ctu_y) {
-  using G = Geo<W, H>;
-  const mip_shape_desc sd = c_shapes[shape];
-  const int modes = sd.modes;             // pairs per CU == modes (2*modes entries)
-  const int njobs = sd.ncu * modes;
-  int job = job0 + lane / G::S;
-  const int sx = lane % G::S, x0 = 4 * sx;
-  const bool active = job < njobs;
-  if (!active) job = njobs - 1;
-  // q-major job order (job = q * ncu + cu): the lanes of a wave share the mode pair, so the
-  // weight-row reads of the matrix products broadcast instead of bank-conflicting.
-  const int q = job / sd.ncu, cu = job - q * sd.ncu;
-  const int cx = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols);
-  const int cy = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
-  const int fx = ctu_x + cx, fy = ctu_y + cy;
-  const bool avail = fx + W <= a.width && fy + H <= a.height;
-
-  // ---- boundaries, intra.cl:96-107 / 232-243 padding, 71-73 / 127-141 downsampling
-  const uint16_t *rt = tile.ref;
-  const int padT = fx > 0 ? rt[tidx(cx - 1, cy)] : 512;      // top edge: sample (x-1, 0)
-  const int padL = fy > 0 ? rt[tidx(cx, cy - 1)] : 512;      // left edge: sample (0, y-1)
-  int redT[G::RBS], redL[G::RBS];
-  {
-    constexpr int dfT = W / G::RBS, l2T = ilog2c(dfT), rndT = dfT > 1 ? dfT / 2 : 0;
-    constexpr int dfL = H / G::RBS, l2L = ilog2c(dfL), rndL = dfL > 1 ? dfL / 2 : 0;
-#pragma unroll
-    for (int i = 0; i < G::RBS; i++) {
-      int s = 0;
-      if (dfT >= 4) {
-#pragma unroll
-        for (int t = 0; t < dfT; t += 4) {
-          const uint2 v = lds_row4(rt, cx + i * dfT + t, cy - 1);
-          s += (v.x & 0xffff) + (v.x >> 16) + (v.y & 0xffff) + (v.y >> 16);
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < dfT; t++) s += rt[tidx(cx + i * dfT + t, cy - 1)];
-      }
-      redT[i] = fy > 0 ? (s + rndT) >> l2T : padT;
-      int l = 0;
-#pragma unroll
-      for (int t = 0; t < dfL; t++) l += rt[tidx(cx - 1, cy + i * dfL + t)];
-      redL[i] = fx > 0 ? (l + rndL) >> l2L : padL;
-    }
-  }
-
-  // ---- MIP input vector, intra.cl:415-454 (pair q: modes 2q, 2q+1; transposed if >= modes)
-  Lane<W, H> L;
-  const int m0 = 2 * q;
-  L.transposed = m0 >= modes;
-  const int mw = L.transposed ? m0 - modes : m0;
-  {
-    int b[8];
-#pragma unroll
-    for (int i = 0; i < G::RBS; i++) {
-      b[i] = L.transposed ? redL[i] : redT[i];
-      b[G::RBS + i] = L.transposed ? redT[i] : redL[i];
-    }
-#pragma unroll
-    for (int i = 2 * G::RBS; i < 8; i++) b[i] = b[0];
-    L.b0 = b[0];
-    int pv[8], psum = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) pv[i] = b[i] - L.b0;
-    pv[0] = G::SID == 2 ? 0 : 512 - L.b0;
-#pragma unroll
-    for (int i = 0; i < 2 * G::RBS; i++) psum += pv[i];
-    L.offset = 32 - 32 * psum;
-#pragma unroll
-    for (int i = 0; i < 4; i++) L.p[i] = s2{(short)pv[2 * i], (short)pv[2 * i + 1]};
-  }
-  L.w0 = tile.w + (G::WROW + mw * G::NOUT) * 8;
-  L.w1 = L.w0 + G::NOUT * 8;
-
+// Packed block results -> 32-bit per-mode accumulators.
+struct Acc {
   uint32_t sad0 = 0, sad1 = 0, satd0 = 0, satd1 = 0;
-  const uint16_t *ot = tile.org;
+  __device__ __forceinline__ void add(u2 sad, u2 satd) {
+    sad0 = __builtin_amdgcn_udot2(sad, (u2){1, 0}, sad0, false);
+    sad1 = __builtin_amdgcn_udot2(sad, (u2){0, 1}, sad1, false);
+    satd0 = __builtin_amdgcn_udot2(satd, (u2){1, 0}, satd0, false);
+    satd1 = __builtin_amdgcn_udot2(satd, (u2){0, 1}, satd1, false);
+  }
+};
 
+struct Ctx {
+  const SearchArgs *a;
+  const uint16_t *org, *ref;  // quadrant tiles (distortion / reference samples)
+  const int16_t *w;           // expanded weights (LDS)
+  uint32_t *wave;             // wave-private LDS: job table + reduced-prediction scratch
+  int ctu, frame, ctu_x, ctu_y, qx, qy;  // qx, qy: quadrant origin inside the CTU
+};
+
+// Horizontal pass of anchor row k (CU row k*UV + UV-1) at strip columns x0..x0+3,
+// intra.cl:816-843; the first UH columns interpolate from the left boundary sample.
+// ((UH-o)*before + o*after + UH/2) >> LH == (base + o*delta) >> LH with
+// base = (before << LH) + UH/2; the sum equals the reference numerator, in [0, 8188].
+template <int W, int H, class RED>
+__device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, int left_k, s2 (&a)[4]) {
+  using G = Geo<W, H>;
+  if constexpr (G::UH == 1) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) a[c] = red(k, x0 + c);
+  } else if constexpr (G::UH == 2) {
+    const int kx = x0 >> 1;  // covers kx, kx+1
+    const s2 r0 = red(k, kx), r1 = red(k, kx + 1);
+    const s2 before = kx == 0 ? splat(left_k) : red(k, max(kx - 1, 0));
+    a[0] = (before + r0 + splat(1)) >> splat(1);
+    a[1] = r0;
+    a[2] = (r0 + r1 + splat(1)) >> splat(1);
+    a[3] = r1;
+  } else {
+    const int kx = x0 >> G::LH;
+    const s2 after = red(k, kx);
+    const s2 before = kx == 0 ? splat(left_k) : red(k, max(kx - 1, 0));
+    const s2 delta = after - before;
+    const s2 base = (before << splat(G::LH)) + splat(G::UH / 2);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int o = ((x0 + c) & (G::UH - 1)) + 1;
+      a[c] = (splat(o) * delta + base) >> splat(G::LH);
+    }
+  }
+}
+
+// Walk one strip of one job: prediction rows (upsampling, intra.cl:815-912) streamed
+// through the block transform.
+template <int W, int H, class RED>
+__device__ __forceinline__ void walk_strip(const Ctx &x, const CuPos &c, const RED &red, int x0, Acc &acc) {
+  using G = Geo<W, H>;
+  const uint16_t *rt = x.ref, *ot = x.org;
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
-    BlockAcc acc;
+    BlockAcc b;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       s2 prow[4];
 #pragma unroll
-      for (int c = 0; c < 4; c++) prow[c] = L.red(i, c);
-      block_row(acc, i, prow, lds_row4(ot, cx, cy + i));
-      __builtin_amdgcn_sched_barrier(0);
+      for (int cc = 0; cc < 4; cc++) prow[cc] = red(i, cc);
+      block_row(b, i, prow, lds_row4(ot, c.lx, c.ly + i));
     }
-    block_finish(acc, sad0, sad1, satd0, satd1);
+    u2 sad, satd;
+    block_finish(b, sad, satd);
+    acc.add(sad, satd);
   } else {
-    // ---- walk the strip downwards, 4x4 block by 4x4 block (intra.cl:815-1117)
-    s2 prev[4], next[4];
+    // Vertical pass (intra.cl:867-893): rows o = 1..UV-1 of window k interpolate between
+    // anchor k-1 (or the top boundary) and anchor k: (base + o*delta) >> LV with
+    // base = (prev << LV) + UV/2, the reference numerator, in [0, 8188].
+    s2 prev[4], next[4], delta[4], base[4];
     {
-      const uint2 tv = fy > 0 ? lds_row4(rt, cx + x0, cy - 1) : make_uint2(0, 0);
+      const uint2 tv = lds_row4(rt, c.lx + x0, c.ly - 1);
       const int t4[4] = {(int)(tv.x & 0xffff), (int)(tv.x >> 16), (int)(tv.y & 0xffff), (int)(tv.y >> 16)};
 #pragma unroll
-      for (int c = 0; c < 4; c++) prev[c] = splat(fy > 0 ? t4[c] : padT);  // refT (vertical "before")
+      for (int cc = 0; cc < 4; cc++) prev[cc] = splat(c.top ? t4[cc] : c.padT);
     }
     int kcur = -1;
 #pragma unroll 1
     for (int by = 0; by < H / 4; by++) {
-      BlockAcc acc;
+      BlockAcc b;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const int y = 4 * by + i;
         s2 prow[4];
         if constexpr (G::UV == 1) {
-          const int leftv = fx > 0 ? rt[tidx(cx - 1, cy + y)] : padL;
-          anchor_row<W, H>(L, y, x0, leftv, prow);
+          const int leftv = c.left ? rt[tidx(c.lx - 1, c.ly + y)] : c.padL;
+          anchor_row<W, H>(red, y, x0, leftv, prow);
         } else {
           const int k = y >> G::LV;
           if (k != kcur) {  // wave-uniform
             if (kcur >= 0) {
 #pragma unroll
-              for (int c = 0; c < 4; c++) prev[c] = next[c];
+              for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
             }
             const int ya = k * G::UV + G::UV - 1;
-            const int leftv = fx > 0 ? rt[tidx(cx - 1, cy + ya)] : padL;
-            anchor_row<W, H>(L, k, x0, leftv, next);
+            const int leftv = c.left ? rt[tidx(c.lx - 1, c.ly + ya)] : c.padL;
+            anchor_row<W, H>(red, k, x0, leftv, next);
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) {
+              delta[cc] = next[cc] - prev[cc];
+              base[cc] = (prev[cc] << splat(G::LV)) + splat(G::UV / 2);
+            }
             kcur = k;
           }
-          const int o = (y & (G::UV - 1)) + 1;  // intra.cl:876-891
+          const int o = (y & (G::UV - 1)) + 1;
 #pragma unroll
-          for (int c = 0; c < 4; c++)
-            prow[c] = o == G::UV ? next[c]
-                                 : prev[c] + ((splat(o) * (next[c] - prev[c]) + splat(G::UV / 2)) >> splat(G::LV));
+          for (int cc = 0; cc < 4; cc++)
+            prow[cc] = o == G::UV ? next[cc] : (splat(o) * delta[cc] + base[cc]) >> splat(G::LV);
         }
-        block_row(acc, i, prow, lds_row4(ot, cx + x0, cy + y));
-        __builtin_amdgcn_sched_barrier(0);
+        block_row(b, i, prow, lds_row4(ot, c.lx + x0, c.ly + y));
       }
-      block_finish(acc, sad0, sad1, satd0, satd1);
+      u2 sad, satd;
+      block_finish(b, sad, satd);
+      acc.add(sad, satd);
     }
-  }
-
-  // ---- combine the strips of one (CU, pair): adjacent lanes, xor-butterfly
-#pragma unroll
-  for (int off = 1; off < G::S; off <<= 1) {
-    sad0 += __shfl_xor(sad0, off);
-    sad1 += __shfl_xor(sad1, off);
-    satd0 += __shfl_xor(satd0, off);
-    satd1 += __shfl_xor(satd1, off);
-  }
-  if (active && sx == 0) {
-    const size_t base = ((size_t)frame * a.nctus + ctu) * MIP_COSTS_PER_CTU + sd.cost_offset +
-                        (size_t)cu * 2 * modes + m0;
-    const int c0 = avail ? min(2 * (int)sad0, (int)satd0) : kUnavailable;  // intra.cl:1166
-    const int c1 = avail ? min(2 * (int)sad1, (int)satd1) : kUnavailable;
-    *reinterpret_cast<int2 *>(a.cost + base) = make_int2(c0, c1);
-    if (a.sad) *reinterpret_cast<int2 *>(a.sad + base) = avail ? make_int2(sad0, sad1) : make_int2(kUnavailable, kUnavailable);
-    if (a.satd) *reinterpret_cast<int2 *>(a.satd + base) = avail ? make_int2(satd0, satd1) : make_int2(kUnavailable, kUnavailable);
   }
 }
 
-// Stage a 129 x 132 window (CTU rows -1..127, columns -4..127) of one frame into LDS.
-// Samples outside the frame read as 0; they only feed CUs whose results are discarded
-// or padding branches that never select them.
+template <int W, int H>
+__device__ __forceinline__ void run_task(const Ctx &x, const WaveTask &task, int lane) {
+  using G = Geo<W, H>;
+  const SearchArgs &a = *x.a;
+  const mip_shape_desc sd = c_shapes[task.shape];
+  const int modes = sd.modes, nj = task.njobs;
+  const Job *jobs = a.jobs + task.job0;
+  const int jl = lane / G::S, sx = lane - jl * G::S, x0 = 4 * sx;
+  const bool active = jl < nj;
+  const Job job = jobs[min(jl, nj - 1)];
+  const CuPos c = cu_pos(sd, job.cu, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
+  Acc acc;
+
+  if constexpr (G::DIRECT) {
+    const MipIn m = mip_inputs<W, H>(c, job.pair, modes, x.ref);
+    auto red = [&](int k, int kx) { return red_direct<W, H>(m, x.w, k, kx); };
+    walk_strip<W, H>(x, c, red, x0, acc);
+  } else {
+    // ---- phase A: each job's reduced prediction once, into the wave's scratch
+    uint32_t *table = x.wave;
+    uint32_t *scr = x.wave + 64 * kJobWords;
+    constexpr int kStride = G::NOUT + 1;  // +1 dword: different jobs hit different banks
+    if (lane < nj) {
+      const Job jb = jobs[lane];
+      const CuPos cj = cu_pos(sd, jb.cu, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
+      const MipIn m = mip_inputs<W, H>(cj, jb.pair, modes, x.ref);
+      uint4 *e = reinterpret_cast<uint4 *>(table + lane * kJobWords);
+      e[0] = make_uint4(as_u32(m.p[0]), as_u32(m.p[1]), as_u32(m.p[2]), as_u32(m.p[3]));
+      e[1] = make_uint4((uint32_t)m.offset, (uint32_t)m.b0, (uint32_t)m.wrow, (uint32_t)m.transposed);
+    }
+    wave_lds_sync();
+    const int total = nj * G::NOUT;
+#pragma unroll 1
+    for (int o = lane; o < ((total + 63) & ~63); o += 64) {
+      const int jb = min(o / G::NOUT, nj - 1), j = o % G::NOUT;
+      const uint4 *e = reinterpret_cast<const uint4 *>(table + jb * kJobWords);
+      const uint4 e0 = e[0], e1 = e[1];
+      const s2 p[4] = {as_s2(e0.x), as_s2(e0.y), as_s2(e0.z), as_s2(e0.w)};
+      const int off = (int)e1.x, b0 = (int)e1.y, wrow = (int)e1.z;
+      const int v0 = gemv<G::SID>(p, x.w + (wrow + j) * 8, off, b0);
+      const int v1 = gemv<G::SID>(p, x.w + (wrow + G::NOUT + j) * 8, off, b0);
+      const int pos = e1.w ? (j % G::R) * G::R + j / G::R : j;
+      if (o < total) scr[jb * kStride + pos] = (uint32_t)v0 | ((uint32_t)v1 << 16);
+    }
+    wave_lds_sync();
+    // ---- phase B
+    const uint32_t *mine = scr + min(jl, nj - 1) * kStride;
+    auto red = [&](int k, int kx) { return as_s2(mine[k * G::R + kx]); };
+    walk_strip<W, H>(x, c, red, x0, acc);
+    wave_lds_sync();  // scratch and table are reused by the next task
+  }
+
+  // ---- combine the strips of one job: adjacent lanes, xor butterfly
+#pragma unroll
+  for (int off = 1; off < G::S; off <<= 1) {
+    acc.sad0 += __shfl_xor(acc.sad0, off);
+    acc.sad1 += __shfl_xor(acc.sad1, off);
+    acc.satd0 += __shfl_xor(acc.satd0, off);
+    acc.satd1 += __shfl_xor(acc.satd1, off);
+  }
+  if (active && sx == 0) {
+    const int fx = x.ctu_x + x.qx + c.lx, fy = x.ctu_y + x.qy + c.ly;
+    const bool avail = fx + W <= a.width && fy + H <= a.height;
+    const size_t idx = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + sd.cost_offset +
+                       (size_t)job.cu * 2 * modes + 2 * job.pair;
+    const int c0 = avail ? min(2 * (int)acc.sad0, (int)acc.satd0) : kUnavailable;  // intra.cl:1166
+    const int c1 = avail ? min(2 * (int)acc.sad1, (int)acc.satd1) : kUnavailable;
+    *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
+    if (a.sad)
+      *reinterpret_cast<int2 *>(a.sad + idx) = avail ? make_int2(acc.sad0, acc.sad1) : make_int2(kUnavailable, kUnavailable);
+    if (a.satd)
+      *reinterpret_cast<int2 *>(a.satd + idx) = avail ? make_int2(acc.satd0, acc.satd1) : make_int2(kUnavailable, kUnavailable);
+  }
+}
+
+// Stage the quadrant window (rows -1..63, columns -4..63) of one frame into LDS.  Samples
+// outside the frame read as 0; they only feed CUs whose results are discarded or padding
+// branches that never select them.
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
-                                           int ctu_x, int ctu_y) {
-  constexpr int kChunks = kPitch / 4;  // 33 chunks of 4 samples per row
-  for (int i = threadIdx.x; i < 129 * kChunks; i += blockDim.x) {
+                                           int x0, int y0) {
+  constexpr int kChunks = kPitch / 4;  // 17 chunks of 4 samples per row
+  for (int i = threadIdx.x; i < 65 * kChunks; i += blockDim.x) {
     const int row = i / kChunks, ch = i - row * kChunks;
-    const int fy = ctu_y - 1 + row, fx = ctu_x - kColOff + 4 * ch;
+    const int fy = y0 - 1 + row, fx = x0 - kColOff + 4 * ch;
     uint2 v = make_uint2(0, 0);
     if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
       v = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
@@ -375,32 +469,33 @@ __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame,
 }
 
 template <bool ALT>
-__global__ __launch_bounds__(256, 3) void mip_search_kernel(SearchArgs a) {
+__global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t *org = smem;
   uint16_t *ref = ALT ? smem + kTileElems : smem;
   int16_t *w = reinterpret_cast<int16_t *>(smem + (ALT ? 2 : 1) * kTileElems);
+  uint32_t *waves = reinterpret_cast<uint32_t *>(w + kWeightWords);
 
-  const int slice = blockIdx.x, ctu = blockIdx.y, frame = blockIdx.z;
+  const int slice = blockIdx.x % a.slices, quad = blockIdx.x / a.slices;
+  const int ctu = blockIdx.y, frame = blockIdx.z;
   const int ctu_x = 128 * (ctu % a.ctu_cols), ctu_y = 128 * (ctu / a.ctu_cols);
+  const int qx = 64 * (quad & 1), qy = 64 * (quad >> 1);
   const size_t fofs = (size_t)frame * a.width * a.height;
 
-  stage_tile(org, a.orig + fofs, a.width, a.height, ctu_x, ctu_y);
-  if (ALT) stage_tile(ref, a.refs + fofs, a.width, a.height, ctu_x, ctu_y);
+  stage_tile(org, a.orig + fofs, a.width, a.height, ctu_x + qx, ctu_y + qy);
+  if (ALT) stage_tile(ref, a.refs + fofs, a.width, a.height, ctu_x + qx, ctu_y + qy);
   for (int i = threadIdx.x; i < kWeightWords / 8; i += blockDim.x)
     reinterpret_cast<uint4 *>(w)[i] = reinterpret_cast<const uint4 *>(a.weights)[i];
   __syncthreads();
 
-  const Tile tile{org, ref, w};
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int stride = 4 * a.slices;
-  for (int t = slice * 4 + wave; t < a.ntasks; t += stride) {
+  const Ctx x{&a, org, ref, w, waves + wave * kWaveWords, ctu, frame, ctu_x, ctu_y, qx, qy};
+  const int t0 = a.task_begin[quad], t1 = a.task_begin[quad + 1];
+  for (int t = t0 + slice * kWaves + wave; t < t1; t += kWaves * a.slices) {
     const WaveTask task = a.tasks[t];
-    const int s = task.shape, j0 = task.job0;
-    // Shapes share code by size class (17 distinct W x H among the 47 shapes).
-    switch (c_shape_class[s]) {
+    switch (c_shape_class[task.shape]) {
 #define MIP_CASE(idx, W, H) \
-  case idx: run_task<W, H>(a, tile, s, j0, lane, ctu, frame, ctu_x, ctu_y); break;
+  case idx: run_task<W, H>(x, task, lane); break;
       MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
       MIP_CASE(4, 32, 8) MIP_CASE(5, 8, 32) MIP_CASE(6, 16, 16) MIP_CASE(7, 16, 8)
       MIP_CASE(8, 8, 16) MIP_CASE(9, 32, 4) MIP_CASE(10, 4, 32) MIP_CASE(11, 16, 4)
@@ -430,15 +525,18 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
 
 }  // namespace
 
-size_t search_lds_bytes(bool alt) { return ((alt ? 2 : 1) * kTileElems + kWeightWords) * 2; }
+size_t search_lds_bytes(bool alt) {
+  return ((alt ? 2 : 1) * kTileElems + kWeightWords) * 2 + (size_t)kWaves * kWaveWords * 4;
+}
 
 hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, hipStream_t s) {
-  const dim3 grid(a.slices, a.nctus, nframes);
+  if (a.slices < 1) return hipErrorInvalidValue;
+  const dim3 grid(4 * a.slices, a.nctus, nframes);
   const size_t lds = search_lds_bytes(alt_refs);
   if (alt_refs)
-    hipLaunchKernelGGL(mip_search_kernel<true>, grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL(mip_search_kernel<true>, grid, dim3(64 * kWaves), lds, s, a);
   else
-    hipLaunchKernelGGL(mip_search_kernel<false>, grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL(mip_search_kernel<false>, grid, dim3(64 * kWaves), lds, s, a);
   return hipGetLastError();
 }
 

@@ -60,35 +60,69 @@ std::vector<int16_t> expand_weights() {
   return w;
 }
 
-// Per-CTU wave-task list: shapes ordered by lane cost (rows per strip, descending) so the
-// round-robin assignment of tasks to waves balances; tasks of one shape stay adjacent so
-// co-resident waves run the same code.
+// Per-quadrant work lists.  Jobs (CU, mode pair) of a shape inside quadrant q are grouped
+// into wave tasks of up to 64/S jobs (S = W/4 strips per CU; at most 16 jobs for shapes
+// that stage reduced predictions in LDS, see mip_search.hip).  Jobs are CU-major for
+// those shapes (lanes of one CU read the same samples) and pair-major for the shapes
+// that compute their matrix products per lane (lanes of a wave share weight rows).
+// Shapes are ordered by rows per strip (descending) so the round-robin assignment of
+// tasks to waves balances, and tasks of one shape stay adjacent.
 // MIPGPU_SHAPE_FILTER="i,j,..." (profiling knob) restricts the search to those shapes.
-std::vector<mipgpu::WaveTask> build_tasks() {
-  std::vector<int> order;
+struct WorkLists {
+  std::vector<mipgpu::WaveTask> tasks;
+  std::vector<mipgpu::Job> jobs;
+  int task_begin[5];
+};
+
+bool shape_selected(int s) {
   const char *flt = getenv("MIPGPU_SHAPE_FILTER");
-  for (int i = 0; i < MIP_NUM_SHAPES; i++) {
-    if (flt && *flt) {
-      bool keep = false;
-      for (const char *p = flt; *p;) {
-        char *end;
-        const long v = strtol(p, &end, 10);
-        if (end == p) break;
-        keep |= v == i;
-        p = *end ? end + 1 : end;
-      }
-      if (!keep) continue;
-    }
-    order.push_back(i);
+  if (!flt || !*flt) return true;
+  for (const char *p = flt; *p;) {
+    char *end;
+    const long v = strtol(p, &end, 10);
+    if (end == p) break;
+    if (v == s) return true;
+    p = *end ? end + 1 : end;
   }
+  return false;
+}
+
+WorkLists build_work() {
+  std::vector<int> order;
+  for (int i = 0; i < MIP_NUM_SHAPES; i++)
+    if (shape_selected(i)) order.push_back(i);
   std::stable_sort(order.begin(), order.end(), [](int a, int b) { return kShapes[a].h > kShapes[b].h; });
-  std::vector<mipgpu::WaveTask> t;
-  for (int s : order) {
-    const int jobs = kShapes[s].ncu * kShapes[s].modes;
-    const int per_task = 64 / (kShapes[s].w / 4);
-    for (int j = 0; j < jobs; j += per_task) t.push_back({(uint16_t)s, (uint16_t)j});
+  WorkLists wl;
+  for (int q = 0; q < 4; q++) {
+    wl.task_begin[q] = (int)wl.tasks.size();
+    for (int s : order) {
+      const mip_shape_desc &sd = kShapes[s];
+      const int r = sd.size_id == 2 ? 8 : 4;
+      const bool direct = sd.w == r;
+      const int strips = sd.w / 4;
+      const int per_task = direct ? 64 / strips : std::min(64 / strips, 16);
+      std::vector<int> cus;
+      for (int cu = 0; cu < sd.ncu; cu++) {
+        const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
+        if (x / 64 == (q & 1) && y / 64 == (q >> 1)) cus.push_back(cu);
+      }
+      std::vector<mipgpu::Job> jobs;
+      if (direct) {
+        for (int p = 0; p < sd.modes; p++)
+          for (int cu : cus) jobs.push_back({(uint16_t)cu, (uint8_t)p, 0});
+      } else {
+        for (int cu : cus)
+          for (int p = 0; p < sd.modes; p++) jobs.push_back({(uint16_t)cu, (uint8_t)p, 0});
+      }
+      for (size_t j = 0; j < jobs.size(); j += per_task) {
+        const int n = (int)std::min<size_t>(per_task, jobs.size() - j);
+        wl.tasks.push_back({(uint8_t)s, (uint8_t)n, 0, (uint32_t)(wl.jobs.size() + j)});
+      }
+      wl.jobs.insert(wl.jobs.end(), jobs.begin(), jobs.end());
+    }
   }
-  return t;
+  wl.task_begin[4] = (int)wl.tasks.size();
+  return wl;
 }
 
 bool filter_supported(int f) { return f == 2 || f == 3 || f == 6 || f == 7; }
@@ -108,7 +142,8 @@ struct mip_engine {
   int32_t *d_costs = nullptr, *d_sad = nullptr, *d_satd = nullptr, *d_best_cost = nullptr;
   uint8_t *d_best = nullptr;
   mipgpu::WaveTask *d_tasks = nullptr;
-  int ntasks = 0;
+  mipgpu::Job *d_jobs = nullptr;
+  int task_begin[5] = {0, 0, 0, 0, 0};
   int16_t *d_weights = nullptr;
   int slices = 8;
 };
@@ -161,7 +196,7 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tasks,
-                  (void *)e->d_weights})
+                  (void *)e->d_jobs, (void *)e->d_weights})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -212,16 +247,19 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   }
   ALLOC(e->d_best, ncu);
   ALLOC(e->d_best_cost, ncu * 4);
-  const std::vector<mipgpu::WaveTask> tasks = build_tasks();
-  e->ntasks = (int)tasks.size();
-  ALLOC(e->d_tasks, tasks.size() * sizeof(mipgpu::WaveTask));
+  const WorkLists wl = build_work();
+  for (int q = 0; q < 5; q++) e->task_begin[q] = wl.task_begin[q];
+  ALLOC(e->d_tasks, std::max<size_t>(1, wl.tasks.size()) * sizeof(mipgpu::WaveTask));
+  ALLOC(e->d_jobs, std::max<size_t>(1, wl.jobs.size()) * sizeof(mipgpu::Job));
   const std::vector<int16_t> w = expand_weights();
   ALLOC(e->d_weights, w.size() * 2);
 #undef ALLOC
-  if (hipMemcpy(e->d_tasks, tasks.data(), tasks.size() * sizeof(mipgpu::WaveTask), hipMemcpyHostToDevice) != hipSuccess ||
+  if ((!wl.tasks.empty() &&
+       (hipMemcpy(e->d_tasks, wl.tasks.data(), wl.tasks.size() * sizeof(mipgpu::WaveTask), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_jobs, wl.jobs.data(), wl.jobs.size() * sizeof(mipgpu::Job), hipMemcpyHostToDevice) != hipSuccess)) ||
       hipMemcpy(e->d_weights, w.data(), w.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail("uploading static tables failed"));
-  e->slices = o.slices_per_ctu > 0 ? o.slices_per_ctu : 8;
+  e->slices = o.slices_per_ctu > 0 ? o.slices_per_ctu : 1;
   *out = e;
   return 0;
 }
@@ -256,12 +294,13 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.sad = d_sad;
   a.satd = d_satd;
   a.tasks = e->d_tasks;
+  a.jobs = e->d_jobs;
   a.weights = e->d_weights;
   a.width = e->width;
   a.height = e->height;
   a.ctu_cols = e->ctu_cols;
   a.nctus = e->nctus;
-  a.ntasks = e->ntasks;
+  for (int q = 0; q < 5; q++) a.task_begin[q] = e->task_begin[q];
   a.slices = e->slices;
   HIP_TRY(mipgpu::launch_search(a, nframes, alt, s));
   if (d_best || d_best_cost) {
