@@ -35,7 +35,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "1080p frames/sec, full MIP mode search over all CU sizes; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E peak (spec)
-VALU_PEAK_OPS = 256 * 128 * 2.4e9  # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz, int32 lane-ops/s
+# VALU: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz = 39.3 T lane-ops/s (a wave64 VALU op issues
+# in 4 cycles, MI355X_MICROARCH.md); the kernel computes in packed int16 (2 ops per lane-op).
+VALU_PEAK_OPS = 256 * 4 * 16 * 2 * 2.4e9
 OPS_PER_CTU = 140.3e6            # SURVEY.md section 8d algorithmic op model
 
 
@@ -193,7 +195,7 @@ def main():
                          "kernel": "mip_search_kernel", "kernel_ms_per_launch": round(max_kernel_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
             "valu": {"achieved": round(ops / (max_kernel_ms * 1e-3) / 1e12, 3), "peak": round(VALU_PEAK_OPS / 1e12, 2),
-                     "unit": "Tops/s (algorithmic int ops, SURVEY 8d model)",
+                     "unit": "Tops/s (algorithmic int ops, SURVEY 8d model; peak = packed-int16 VALU rate)",
                      "frac": round(ops / (max_kernel_ms * 1e-3) / VALU_PEAK_OPS, 4)},
         }
         if world == 1:

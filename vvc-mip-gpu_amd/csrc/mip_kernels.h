@@ -9,11 +9,14 @@ namespace mipgpu {
 // Work is organised per 64x64 quadrant of a CTU (no CU of the 47 shapes straddles a
 // quadrant).  A *job* is one (CU, mode pair) of a shape inside the quadrant; a *wave task*
 // is up to 64/S jobs of one shape (S = W/4 strips per CU), one lane per (job, strip).
+// Job geometry is resolved on the host (no integer division in the kernel).
 struct Job {
-  uint16_t cu;    // CU index within its shape (reference order, constants.h:1235-1354)
-  uint8_t pair;   // mode pair q: modes 2q, 2q+1 (transposed when 2q >= modes)
-  uint8_t pad;
+  uint32_t cost;  // entry of mode 2q inside the CTU's cost block: shape offset + cu*2*modes + 2q
+                  // (CU index in reference order, constants.h:1235-1354 / 1558-1631)
+  uint8_t lx, ly; // CU origin inside the 64x64 quadrant
+  uint16_t wrow;  // weight row of mode (2q mod modes); bit 15: pair is transposed (2q >= modes)
 };
+constexpr uint16_t kJobTransposed = 0x8000;
 struct WaveTask {
   uint8_t shape;
   uint8_t njobs;

@@ -56,16 +56,13 @@ constexpr int kUnavailable = 0x7fffffff;
 __device__ __forceinline__ int tidx(int x, int y) { return (y + 1) * kPitch + x + kColOff; }
 __device__ __forceinline__ s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
 __device__ __forceinline__ u2 as_u2(s2 v) { return __builtin_bit_cast(u2, v); }
+__device__ __forceinline__ s2 as_s2(u2 v) { return __builtin_bit_cast(s2, v); }
 __device__ __forceinline__ uint32_t as_u32(s2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ s2 splat(int v) { return s2{(short)v, (short)v}; }
 __device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ s2 smin(s2 a, s2 b) { return __builtin_elementwise_min(a, b); }
 
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
-
-__device__ __forceinline__ int axis_pos(int base, int step, int dual, int i) {
-  return dual ? base + (i >> 1) * step + (i & 1) * dual : base + i * step;
-}
 
 // LDS fence for data handed between lanes of ONE wave (wave-private scratch).
 __device__ __forceinline__ void wave_lds_sync() {
@@ -85,7 +82,6 @@ struct Geo {
   static constexpr int LH = ilog2c(UH), LV = ilog2c(UV);
   static constexpr int S = W / 4;                     // strips per CU
   static constexpr bool DIRECT = UH == 1;             // no reduced value shared by strips
-  static constexpr int WROW = SID == 2 ? 0 : (SID == 1 ? kWeightRowOffS1 : kWeightRowOffS0);
 };
 
 // Matrix-vector product of one mode for output j, intra.cl:449-482: ((offset + p.w) >> 6)
@@ -111,7 +107,7 @@ __device__ __forceinline__ int gemv(const s2 (&p)[4], const int16_t *wrow, int o
 struct MipIn {
   s2 p[4];
   int offset, b0;
-  int wrow;        // first weight row (16-B rows) of mode 2q mod modes
+  int wrow;        // first weight row (16-B rows) of mode 2q mod modes (Job::wrow)
   bool transposed;
 };
 
@@ -122,22 +118,16 @@ struct CuPos {
   int padT, padL;  // padding values, intra.cl:102-106, 238-242
 };
 
-__device__ __forceinline__ CuPos cu_pos(const mip_shape_desc &sd, int cu, int ctu_x, int ctu_y, int qx, int qy,
-                                        const uint16_t *rt);
-
 __device__ __forceinline__ uint2 lds_row4(const uint16_t *tile, int x, int y) {
   return *reinterpret_cast<const uint2 *>(tile + tidx(x, y));
 }
 
-__device__ __forceinline__ CuPos cu_pos(const mip_shape_desc &sd, int cu, int ctu_x, int ctu_y, int qx, int qy,
-                                        const uint16_t *rt) {
+__device__ __forceinline__ CuPos cu_pos(const Job &j, int ctu_x, int ctu_y, int qx, int qy, const uint16_t *rt) {
   CuPos c;
-  const int cx = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols);
-  const int cy = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
-  c.lx = cx - qx;
-  c.ly = cy - qy;
-  c.top = ctu_y + cy > 0;
-  c.left = ctu_x + cx > 0;
+  c.lx = j.lx;
+  c.ly = j.ly;
+  c.top = ctu_y + qy + c.ly > 0;
+  c.left = ctu_x + qx + c.lx > 0;
   c.padT = c.left ? rt[tidx(c.lx - 1, c.ly)] : 512;   // top edge: sample (x-1, 0)
   c.padL = c.top ? rt[tidx(c.lx, c.ly - 1)] : 512;    // left edge: sample (0, y-1)
   return c;
@@ -146,7 +136,7 @@ __device__ __forceinline__ CuPos cu_pos(const mip_shape_desc &sd, int cu, int ct
 // Reduced boundaries and MIP input vector of one job, intra.cl:71-73, 127-141, 202-204,
 // 259-279 (box downsampling; a factor of 1 is a copy) and intra.cl:415-454.
 template <int W, int H>
-__device__ __forceinline__ MipIn mip_inputs(const CuPos &c, int pair, int modes, const uint16_t *rt) {
+__device__ __forceinline__ MipIn mip_inputs(const CuPos &c, uint32_t wrow, const uint16_t *rt) {
   using G = Geo<W, H>;
   constexpr int dfT = W / G::RBS, l2T = ilog2c(dfT), rndT = dfT > 1 ? dfT / 2 : 0;
   constexpr int dfL = H / G::RBS, l2L = ilog2c(dfL), rndL = dfL > 1 ? dfL / 2 : 0;
@@ -171,9 +161,8 @@ __device__ __forceinline__ MipIn mip_inputs(const CuPos &c, int pair, int modes,
     redL[i] = c.left ? (l + rndL) >> l2L : c.padL;
   }
   MipIn m;
-  const int m0 = 2 * pair;
-  m.transposed = m0 >= modes;
-  const int mw = m.transposed ? m0 - modes : m0;
+  m.transposed = (wrow & kJobTransposed) != 0;
+  m.wrow = wrow & ~(uint32_t)kJobTransposed;
   int b[8];
 #pragma unroll
   for (int i = 0; i < G::RBS; i++) {
@@ -192,7 +181,6 @@ __device__ __forceinline__ MipIn mip_inputs(const CuPos &c, int pair, int modes,
   m.offset = 32 - 32 * psum;             // intra.cl:449-454
 #pragma unroll
   for (int i = 0; i < 4; i++) m.p[i] = s2{(short)pv[2 * i], (short)pv[2 * i + 1]};
-  m.wrow = G::WROW + mw * G::NOUT;
   return m;
 }
 
@@ -306,11 +294,14 @@ __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, int le
 }
 
 // Walk one strip of one job: prediction rows (upsampling, intra.cl:815-912) streamed
-// through the block transform.
+// through the block transform.  The loops follow the upsampling windows, so every
+// interpolation weight is a compile-time constant (or a wave-uniform loop index).
 template <int W, int H, class RED>
 __device__ __forceinline__ void walk_strip(const Ctx &x, const CuPos &c, const RED &red, int x0, Acc &acc) {
   using G = Geo<W, H>;
   const uint16_t *rt = x.ref, *ot = x.org;
+  auto left_at = [&](int y) { return c.left ? (int)rt[tidx(c.lx - 1, c.ly + y)] : c.padL; };
+  auto orow = [&](int y) { return lds_row4(ot, c.lx + x0, c.ly + y); };
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
     BlockAcc b;
@@ -319,60 +310,89 @@ __device__ __forceinline__ void walk_strip(const Ctx &x, const CuPos &c, const R
       s2 prow[4];
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) prow[cc] = red(i, cc);
-      block_row(b, i, prow, lds_row4(ot, c.lx, c.ly + i));
+      block_row(b, i, prow, orow(i));
     }
     u2 sad, satd;
     block_finish(b, sad, satd);
     acc.add(sad, satd);
+  } else if constexpr (G::UV == 1) {
+    // every row is an anchor row (horizontal pass only)
+#pragma unroll 1
+    for (int by = 0; by < H / 4; by++) {
+      BlockAcc b;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        s2 prow[4];
+        anchor_row<W, H>(red, 4 * by + i, x0, left_at(4 * by + i), prow);
+        block_row(b, i, prow, orow(4 * by + i));
+      }
+      u2 sad, satd;
+      block_finish(b, sad, satd);
+      acc.add(sad, satd);
+    }
   } else {
-    // Vertical pass (intra.cl:867-893): rows o = 1..UV-1 of window k interpolate between
+    // Vertical pass (intra.cl:867-893): row o (1..UV) of window k interpolates between
     // anchor k-1 (or the top boundary) and anchor k: (base + o*delta) >> LV with
-    // base = (prev << LV) + UV/2, the reference numerator, in [0, 8188].
-    s2 prev[4], next[4], delta[4], base[4];
+    // base = (prev << LV) + UV/2, the reference numerator, in [0, 8188]; o = UV gives the
+    // anchor itself.  16-bit wrap-around in o*delta cancels in the in-range sum.
+    s2 prev[4];
     {
       const uint2 tv = lds_row4(rt, c.lx + x0, c.ly - 1);
       const int t4[4] = {(int)(tv.x & 0xffff), (int)(tv.x >> 16), (int)(tv.y & 0xffff), (int)(tv.y >> 16)};
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) prev[cc] = splat(c.top ? t4[cc] : c.padT);
     }
-    int kcur = -1;
+    if constexpr (G::UV == 2) {
+      // two windows per 4x4 block
 #pragma unroll 1
-    for (int by = 0; by < H / 4; by++) {
-      BlockAcc b;
+      for (int by = 0; by < H / 4; by++) {
+        BlockAcc b;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int y = 4 * by + i;
-        s2 prow[4];
-        if constexpr (G::UV == 1) {
-          const int leftv = c.left ? rt[tidx(c.lx - 1, c.ly + y)] : c.padL;
-          anchor_row<W, H>(red, y, x0, leftv, prow);
-        } else {
-          const int k = y >> G::LV;
-          if (k != kcur) {  // wave-uniform
-            if (kcur >= 0) {
+        for (int h = 0; h < 2; h++) {
+          const int k = 2 * by + h;
+          s2 next[4], mid[4];
+          anchor_row<W, H>(red, k, x0, left_at(2 * k + 1), next);
 #pragma unroll
-              for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
-            }
-            const int ya = k * G::UV + G::UV - 1;
-            const int leftv = c.left ? rt[tidx(c.lx - 1, c.ly + ya)] : c.padL;
-            anchor_row<W, H>(red, k, x0, leftv, next);
+          for (int cc = 0; cc < 4; cc++) mid[cc] = as_s2((as_u2(prev[cc]) + as_u2(next[cc]) + (u2){1, 1}) >> (u2){1, 1});
+          block_row(b, 2 * h, mid, orow(2 * k));
+          block_row(b, 2 * h + 1, next, orow(2 * k + 1));
 #pragma unroll
-            for (int cc = 0; cc < 4; cc++) {
-              delta[cc] = next[cc] - prev[cc];
-              base[cc] = (prev[cc] << splat(G::LV)) + splat(G::UV / 2);
-            }
-            kcur = k;
-          }
-          const int o = (y & (G::UV - 1)) + 1;
-#pragma unroll
-          for (int cc = 0; cc < 4; cc++)
-            prow[cc] = o == G::UV ? next[cc] : (splat(o) * delta[cc] + base[cc]) >> splat(G::LV);
+          for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
         }
-        block_row(b, i, prow, lds_row4(ot, c.lx + x0, c.ly + y));
+        u2 sad, satd;
+        block_finish(b, sad, satd);
+        acc.add(sad, satd);
       }
-      u2 sad, satd;
-      block_finish(b, sad, satd);
-      acc.add(sad, satd);
+    } else {
+      constexpr int NB = G::UV / 4;  // blocks per window
+#pragma unroll 1
+      for (int k = 0; k < G::R; k++) {
+        s2 next[4];
+        anchor_row<W, H>(red, k, x0, left_at(k * G::UV + G::UV - 1), next);
+        u2 delta[4], base[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+          delta[cc] = as_u2(next[cc]) - as_u2(prev[cc]);
+          base[cc] = (as_u2(prev[cc]) << (u2){G::LV, G::LV}) + (u2){G::UV / 2, G::UV / 2};
+        }
+#pragma unroll 2
+        for (int bi = 0; bi < NB; bi++) {
+          BlockAcc b;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const unsigned short o = (unsigned short)(4 * bi + i + 1);
+            s2 prow[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) prow[cc] = as_s2(((u2){o, o} * delta[cc] + base[cc]) >> (u2){G::LV, G::LV});
+            block_row(b, i, prow, orow(k * G::UV + 4 * bi + i));
+          }
+          u2 sad, satd;
+          block_finish(b, sad, satd);
+          acc.add(sad, satd);
+        }
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
+      }
     }
   }
 }
@@ -381,17 +401,16 @@ template <int W, int H>
 __device__ __forceinline__ void run_task(const Ctx &x, const WaveTask &task, int lane) {
   using G = Geo<W, H>;
   const SearchArgs &a = *x.a;
-  const mip_shape_desc sd = c_shapes[task.shape];
-  const int modes = sd.modes, nj = task.njobs;
+  const int nj = task.njobs;
   const Job *jobs = a.jobs + task.job0;
   const int jl = lane / G::S, sx = lane - jl * G::S, x0 = 4 * sx;
   const bool active = jl < nj;
   const Job job = jobs[min(jl, nj - 1)];
-  const CuPos c = cu_pos(sd, job.cu, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
+  const CuPos c = cu_pos(job, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
   Acc acc;
 
   if constexpr (G::DIRECT) {
-    const MipIn m = mip_inputs<W, H>(c, job.pair, modes, x.ref);
+    const MipIn m = mip_inputs<W, H>(c, job.wrow, x.ref);
     auto red = [&](int k, int kx) { return red_direct<W, H>(m, x.w, k, kx); };
     walk_strip<W, H>(x, c, red, x0, acc);
   } else {
@@ -401,8 +420,8 @@ __device__ __forceinline__ void run_task(const Ctx &x, const WaveTask &task, int
     constexpr int kStride = G::NOUT + 1;  // +1 dword: different jobs hit different banks
     if (lane < nj) {
       const Job jb = jobs[lane];
-      const CuPos cj = cu_pos(sd, jb.cu, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
-      const MipIn m = mip_inputs<W, H>(cj, jb.pair, modes, x.ref);
+      const CuPos cj = cu_pos(jb, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
+      const MipIn m = mip_inputs<W, H>(cj, jb.wrow, x.ref);
       uint4 *e = reinterpret_cast<uint4 *>(table + lane * kJobWords);
       e[0] = make_uint4(as_u32(m.p[0]), as_u32(m.p[1]), as_u32(m.p[2]), as_u32(m.p[3]));
       e[1] = make_uint4((uint32_t)m.offset, (uint32_t)m.b0, (uint32_t)m.wrow, (uint32_t)m.transposed);
@@ -440,8 +459,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const WaveTask &task, int
   if (active && sx == 0) {
     const int fx = x.ctu_x + x.qx + c.lx, fy = x.ctu_y + x.qy + c.ly;
     const bool avail = fx + W <= a.width && fy + H <= a.height;
-    const size_t idx = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + sd.cost_offset +
-                       (size_t)job.cu * 2 * modes + 2 * job.pair;
+    const size_t idx = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
     const int c0 = avail ? min(2 * (int)acc.sad0, (int)acc.satd0) : kUnavailable;  // intra.cl:1166
     const int c1 = avail ? min(2 * (int)acc.sad1, (int)acc.satd1) : kUnavailable;
     *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);

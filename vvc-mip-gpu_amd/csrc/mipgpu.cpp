@@ -100,19 +100,29 @@ WorkLists build_work() {
       const int r = sd.size_id == 2 ? 8 : 4;
       const bool direct = sd.w == r;
       const int strips = sd.w / 4;
-      const int per_task = direct ? 64 / strips : std::min(64 / strips, 16);
+      // shapes staging reduced predictions: the wave scratch holds 16 x 65 dwords
+      const int per_task = direct ? 64 / strips : std::min(64 / strips, 1040 / (r * r + 1));
       std::vector<int> cus;
       for (int cu = 0; cu < sd.ncu; cu++) {
         const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
         if (x / 64 == (q & 1) && y / 64 == (q >> 1)) cus.push_back(cu);
       }
+      const int nout = r * r;
+      const int wrow0 = sd.size_id == 2 ? 0 : (sd.size_id == 1 ? mipgpu::kWeightRowOffS1 : mipgpu::kWeightRowOffS0);
+      auto make_job = [&](int cu, int p) {
+        const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
+        const bool tr = 2 * p >= sd.modes;
+        const int mw = tr ? 2 * p - sd.modes : 2 * p;
+        return mipgpu::Job{(uint32_t)(sd.cost_offset + cu * 2 * sd.modes + 2 * p), (uint8_t)(x % 64), (uint8_t)(y % 64),
+                           (uint16_t)((wrow0 + mw * nout) | (tr ? mipgpu::kJobTransposed : 0))};
+      };
       std::vector<mipgpu::Job> jobs;
       if (direct) {
         for (int p = 0; p < sd.modes; p++)
-          for (int cu : cus) jobs.push_back({(uint16_t)cu, (uint8_t)p, 0});
+          for (int cu : cus) jobs.push_back(make_job(cu, p));
       } else {
         for (int cu : cus)
-          for (int p = 0; p < sd.modes; p++) jobs.push_back({(uint16_t)cu, (uint8_t)p, 0});
+          for (int p = 0; p < sd.modes; p++) jobs.push_back(make_job(cu, p));
       }
       for (size_t j = 0; j < jobs.size(); j += per_task) {
         const int n = (int)std::min<size_t>(per_task, jobs.size() - j);
