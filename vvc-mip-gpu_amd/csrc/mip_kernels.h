@@ -7,22 +7,39 @@
 namespace mipgpu {
 
 // Work is organised per 64x64 quadrant of a CTU (no CU of the 47 shapes straddles a
-// quadrant).  A *job* is one (CU, mode pair) of a shape inside the quadrant; a *wave task*
-// is up to 64/S jobs of one shape (S = W/4 strips per CU), one lane per (job, strip).
-// Job geometry is resolved on the host (no integer division in the kernel).
-struct Job {
-  uint32_t cost;  // entry of mode 2q inside the CTU's cost block: shape offset + cu*2*modes + 2q
+// quadrant).  CUs of one size class (W x H; several shapes share a class) are grouped into
+// wave *tasks*: up to 64/(S*V) CUs (S = W/4 column strips, V = row parts, see
+// mip_search.hip) and a range of mode pairs; one lane per (CU, strip, row part) walks
+// the pairs one after another.
+struct Job {      // one CU of a task (geometry resolved on the host: no division in kernels)
+  uint32_t cost;  // entry of mode 0 inside the CTU's cost block: shape offset + cu*2*modes
                   // (CU index in reference order, constants.h:1235-1354 / 1558-1631)
   uint8_t lx, ly; // CU origin inside the 64x64 quadrant
-  uint16_t wrow;  // weight row of mode (2q mod modes); bit 15: pair is transposed (2q >= modes)
-};
-constexpr uint16_t kJobTransposed = 0x8000;
-struct WaveTask {
-  uint8_t shape;
-  uint8_t njobs;
   uint16_t pad;
-  uint32_t job0;  // index into the quadrant's job array
 };
+struct WaveTask {
+  uint8_t cls;    // size class, kClassW/kClassH
+  uint8_t ncu;    // CUs in the task
+  uint8_t q0, q1; // mode pairs [q0, q1): pair q = modes 2q, 2q+1 (transposed when 2q >= modes)
+  uint32_t cu0;   // first CU in the job array
+};
+
+constexpr int kNumClasses = 17;
+constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 16, 4, 8, 8, 4, 4};
+constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4};
+constexpr int size_class(int w, int h) {
+  for (int i = 0; i < kNumClasses; i++)
+    if (kClassW[i] == w && kClassH[i] == h) return i;
+  return -1;
+}
+constexpr int class_size_id(int w, int h) { return (w == 4 && h == 4) ? 0 : ((w == 4 || h == 4 || (w == 8 && h == 8)) ? 1 : 2); }
+// Row parts: classes with few CUs per quadrant split each CU's rows over V lanes per strip
+// so that a task still fills the wave.
+constexpr int class_row_parts(int w, int h) {
+  return (w == 64 || (w == 16 && h == 32)) ? 4
+         : ((w == 32 && h >= 8) || (w == 4 && h >= 16)) ? 2 : 1;
+}
+constexpr int class_slots(int w, int h) { return 64 / ((w / 4) * class_row_parts(w, h)); }
 
 struct SearchArgs {
   const uint16_t *orig;   // [frames][height][width] original samples (distortion)
@@ -30,22 +47,25 @@ struct SearchArgs {
   int32_t *cost;          // [frames][nctus][97840]  min(2*SAD, SATD)
   int32_t *sad;           // optional, same layout
   int32_t *satd;          // optional, same layout
-  const WaveTask *tasks;  // 4 per-quadrant task lists, concatenated (heaviest first)
-  const Job *jobs;        // 4 per-quadrant job arrays, concatenated
-  const int16_t *weights; // expanded MIP weights, see kWeightWords
+  const WaveTask *tasks;  // per (quadrant, wave) task lists, concatenated
+  const Job *jobs;
+  const int *list_begin;  // task list of (quadrant q, bin b): [list_begin[q*bins+b], list_begin[q*bins+b+1])
+  const uint4 *tables;    // kTableBytes: MIP matrices for the MFMA, see below
   int width, height;
   int ctu_cols, nctus;
-  int task_begin[5];      // quadrant q's tasks: [task_begin[q], task_begin[q+1])
   int slices;             // workgroups per CTU quadrant
+  int bins;               // task lists per quadrant (= slices * waves per workgroup)
 };
 
-// Expanded weight table (int16): 16-byte rows of 8 taps, index (mode*outputs + j)*8.
-//   sizeId 2: rows [0, 384)    taps (0, w0..w6)   (mip_matrix.cl:441, intra.cl:459-463)
-//   sizeId 1: rows [384, 512)  taps w0..w7
-//   sizeId 0: rows [512, 768)  taps w0..w3, 0, 0, 0, 0
-constexpr int kWeightRowsS2 = 6 * 64, kWeightRowsS1 = 8 * 16, kWeightRowsS0 = 16 * 16;
-constexpr int kWeightRowOffS1 = kWeightRowsS2, kWeightRowOffS0 = kWeightRowsS2 + kWeightRowsS1;
-constexpr int kWeightWords = (kWeightRowsS2 + kWeightRowsS1 + kWeightRowsS0) * 8;
+// MIP matrices, restated for an exact f16 MFMA (mip_search.hip, phase A):
+//   f16 rows [768][8], row = base(sizeId) + mode*R*R + j, base = 0 / 384 / 512 for sizeId
+//   2 / 1 / 0.  Half k is the coefficient of input k: input 0 carries b0 with (96 - w0)/64,
+//   inputs k >= 1 carry p_k with (w_k - 32)/64 (sizeId 2 uses the shifted columns
+//   (w0 := 32, w_1..7 = mip_matrix.cl:441 columns 0..6); sizeId 0 has 4 inputs).
+//   f32 rows [384] (sizeId 1 and 0, from row 384): accumulator init 8*(w0 - 32) + 0.5.
+constexpr int kWeightRows = 768, kWeightRowOffS1 = 384, kWeightRowOffS0 = 512;
+constexpr int kCtabRows = 384;
+constexpr int kTableBytes = kWeightRows * 16 + kCtabRows * 4;
 
 struct BestArgs {
   const int32_t *cost;
@@ -62,6 +82,7 @@ struct FilterArgs {
   int kernel_idx;
 };
 
+int search_waves_per_group();
 hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, hipStream_t s);
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s);

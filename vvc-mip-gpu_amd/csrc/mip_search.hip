@@ -7,21 +7,21 @@
 // ~1.2 GB of reduced predictions per 1080p frame, main.cpp:443-444).
 //
 // Work decomposition
-//   workgroup = (CTU quadrant, slice), kWaves waves.  No CU of the 47 shapes straddles a
-//               64x64 quadrant, so a workgroup stages only its quadrant (+1 row above,
-//               +4 columns left: the reference samples) in LDS, 8.8 KB.
-//   wave      = one WaveTask: up to 64/S jobs (CU, mode pair) of ONE shape, so every
-//               loop bound and branch is wave-uniform.
-//   lane      = (job, 4-column strip).  The two modes of a pair travel in the two 16-bit
-//               halves of each VGPR: upsampling, SAD and the Hadamard are packed int16
-//               VALU ops (v_pk_*); all intermediates provably fit 16 bits (bounds inline).
-//   Phase A   (shapes whose strips share reduced-prediction values, W > R): the wave
-//               computes each job's reduced prediction once (v_dot2_i32_i16) into a
-//               wave-private LDS scratch in the reference's stored order.
-//   Phase B   every lane walks its strip 4x4 block by 4x4 block: anchors (horizontal
-//               pass), vertical interpolation, SAD and SATD; strips of one job are adjacent
-//               lanes and are combined with xor shuffles.  Shapes with W == R (no sharing)
-//               compute their matrix products directly in phase B.
+//   workgroup = (CTU quadrant, slice), 8 waves.  No CU of the 47 shapes straddles a 64x64
+//               quadrant, so a workgroup stages only its quadrant (+1 row above, +4 columns
+//               left: the reference samples) and the MIP matrices in LDS.
+//   wave      = a list of tasks (host-built, load balanced).  A task is up to 64/(S*V) CUs
+//               of ONE size class W x H (S = W/4 column strips, V = row parts) and a range
+//               of mode pairs; every loop bound is a compile-time constant of the class.
+//   lane      = (CU, row part, strip), CU-stationary: it loads its boundaries and original
+//               samples once and walks the mode pairs of the task one after another.  The
+//               two modes of a pair ride in the two 16-bit halves of each VGPR (packed
+//               v_pk_* int16 ops; all intermediates provably fit 16 bits).
+//   per pair  phase A: the reduced predictions of all CUs of the task for the pair, as
+//               16x16x16 f16 MFMAs (exact: integer inputs < 2^11, sums < 2^24), into a
+//               wave-private LDS scratch; phase B: every lane upsamples its strip window by
+//               window and computes SAD + SATD 4x4 block by 4x4 block; strips and row parts
+//               of a CU are combined with xor shuffles, one lane stores the two costs.
 //
 // Bit-exactness: every step restates the reference integer semantics (citations inline);
 // tests/test_gpu_parity.py checks the tables bit for bit against the C oracle, which is
@@ -34,30 +34,36 @@ namespace {
 
 typedef short __attribute__((ext_vector_type(2))) s2;
 typedef unsigned short __attribute__((ext_vector_type(2))) u2;
+typedef _Float16 __attribute__((ext_vector_type(2))) h2;
+typedef _Float16 __attribute__((ext_vector_type(4))) h4;
+typedef float __attribute__((ext_vector_type(4))) f4;
 
 __constant__ mip_shape_desc c_shapes[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;
-// Size class of each shape (index into the run_task<W, H> instantiations).
-__constant__ uint8_t c_shape_class[MIP_NUM_SHAPES] = {
-    0, 1, 2, 3, 4, 5, 6, 7, 8,                                  // aligned SizeId 2
-    2, 3, 4, 4, 5, 5, 6, 6, 6, 7, 7, 7, 7, 7, 8, 8, 8, 8, 8,    // NA SizeId 2
-    9, 10, 11, 12, 13, 14, 14, 15, 15,                          // aligned SizeId 1
-    11, 12, 13, 13, 13, 13, 13, 14, 15,                         // NA SizeId 1
-    16};                                                        // 4x4
+
+#ifndef MIP_ONLY_CLASS
+#define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
+#endif
 
 constexpr int kWaves = 8;        // waves per workgroup
 constexpr int kPitch = 68;       // LDS row pitch in samples (34 dwords: conflict-free rows)
 constexpr int kColOff = 4;       // LDS column of quadrant column 0 (-4..-1: left halo)
 constexpr int kTileElems = (65 * kPitch + 7) / 8 * 8;  // quadrant rows -1..63
-constexpr int kJobWords = 8;     // job-table entry (dwords)
-constexpr int kScratchWords = 16 * 65;                  // 16 jobs x (64 + 1) packed pairs
-constexpr int kWaveWords = 64 * kJobWords + kScratchWords;
+// Alternative references (ALT): CU boundaries only read quadrant rows 4i-1 (top) and
+// columns 4i-1 (left), so only that lattice of the reference frame is staged.
+constexpr int kLatRowPitch = kPitch, kLatColPitch = 66;
+constexpr int kLatElems = (16 * kLatRowPitch + 16 * kLatColPitch + 7) / 8 * 8;
+// Wave-private LDS: per-CU MFMA inputs + reduced-prediction scratch.
+constexpr int kEntryBytes = 32;                         // 2 orientations x 8 f16 inputs
+constexpr int kCuTableBytes = 64 * kEntryBytes;
+constexpr int kScratchWords = 1024;                     // [position][slot] packed mode pairs
+constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
+constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 32;    // > every uniform B offset + 8 B
 constexpr int kUnavailable = 0x7fffffff;
 
 __device__ __forceinline__ int tidx(int x, int y) { return (y + 1) * kPitch + x + kColOff; }
 __device__ __forceinline__ s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
 __device__ __forceinline__ u2 as_u2(s2 v) { return __builtin_bit_cast(u2, v); }
 __device__ __forceinline__ s2 as_s2(u2 v) { return __builtin_bit_cast(s2, v); }
-__device__ __forceinline__ uint32_t as_u32(s2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ s2 splat(int v) { return s2{(short)v, (short)v}; }
 __device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ s2 smin(s2 a, s2 b) { return __builtin_elementwise_min(a, b); }
@@ -71,45 +77,49 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Compile-time geometry of a CU shape (W x H).
+// Compile-time geometry of a size class (W x H).
 template <int W, int H>
 struct Geo {
-  static constexpr int SID = (W == 4 && H == 4) ? 0 : ((W == 4 || H == 4 || (W == 8 && H == 8)) ? 1 : 2);
+  static constexpr int SID = class_size_id(W, H);
   static constexpr int R = SID == 2 ? 8 : 4;          // reduced prediction side
   static constexpr int RBS = SID == 0 ? 2 : 4;        // reduced boundary length per side
   static constexpr int NOUT = R * R;
   static constexpr int UH = W / R, UV = H / R;        // upsampling factors
   static constexpr int LH = ilog2c(UH), LV = ilog2c(UV);
-  static constexpr int S = W / 4;                     // strips per CU
-  static constexpr bool DIRECT = UH == 1;             // no reduced value shared by strips
+  static constexpr int S = W / 4;                     // column strips per CU
+  static constexpr int V = class_row_parts(W, H);     // row parts per CU
+  static constexpr int SLOTS = class_slots(W, H);     // CUs per task
+  static constexpr int KV = R / V;                    // upsampling windows per row part
+  static constexpr bool CHUNKED = SID == 2 && UH == 1;  // 8xH: reduced rows in two halves
+  static constexpr int CPOS = CHUNKED ? 32 : NOUT;    // scratch positions per chunk
+  static constexpr int WBASE = SID == 2 ? 0 : (SID == 1 ? kWeightRowOffS1 : kWeightRowOffS0);
+  static constexpr int MODES = SID == 2 ? 6 : (SID == 1 ? 8 : 16);
+  static_assert(SLOTS * S * V == 64, "lanes");
+  static_assert(CPOS * SLOTS <= kScratchWords, "scratch");
+  // a row part is whole upsampling windows and whole 4x4 blocks
+  static_assert(V == 1 || (!CHUNKED && SID != 0 && (UV >= 4 || KV % (4 / UV) == 0)), "row parts");
 };
 
-// Matrix-vector product of one mode for output j, intra.cl:449-482: ((offset + p.w) >> 6)
-// + b0, clipped to 10 bits.  All operands are small integers, v_dot2_i32_i16 is exact.
-template <int SID>
-__device__ __forceinline__ int gemv(const s2 (&p)[4], const int16_t *wrow, int offset, int b0) {
-  int acc = offset;
-  if (SID == 0) {
-    const uint2 w = *reinterpret_cast<const uint2 *>(wrow);
-    acc = __builtin_amdgcn_sdot2(p[0], as_s2(w.x), acc, false);
-    acc = __builtin_amdgcn_sdot2(p[1], as_s2(w.y), acc, false);
-  } else {
-    const uint4 w = *reinterpret_cast<const uint4 *>(wrow);
-    acc = __builtin_amdgcn_sdot2(p[0], as_s2(w.x), acc, false);
-    acc = __builtin_amdgcn_sdot2(p[1], as_s2(w.y), acc, false);
-    acc = __builtin_amdgcn_sdot2(p[2], as_s2(w.z), acc, false);
-    acc = __builtin_amdgcn_sdot2(p[3], as_s2(w.w), acc, false);
+// ---- reference samples -------------------------------------------------------------
+// Full quadrant tile (original references): any (x, y) of rows -1..63, columns -4..63.
+// Lattice (ALT): rows y = 4i-1 and columns x = 4i-1 only -- all a CU boundary reads.
+template <bool LAT>
+struct RefTile {
+  const uint16_t *t;
+  __device__ __forceinline__ int top(int x, int y) const {      // y = 4i - 1
+    return LAT ? t[((y + 1) >> 2) * kLatRowPitch + x + kColOff] : t[tidx(x, y)];
   }
-  return min(max((acc >> 6) + b0, 0), 1023);
-}
-
-// MIP inputs of one job: packed p vector, offset, b0, weight rows of its two modes.
-struct MipIn {
-  s2 p[4];
-  int offset, b0;
-  int wrow;        // first weight row (16-B rows) of mode 2q mod modes (Job::wrow)
-  bool transposed;
+  __device__ __forceinline__ uint2 top4(int x, int y) const {   // y = 4i - 1, x = 4k
+    return *reinterpret_cast<const uint2 *>(t + (LAT ? ((y + 1) >> 2) * kLatRowPitch + x + kColOff : tidx(x, y)));
+  }
+  __device__ __forceinline__ int left(int x, int y) const {     // x = 4i - 1
+    return LAT ? t[16 * kLatRowPitch + ((x + 1) >> 2) * kLatColPitch + y + 1] : t[tidx(x, y)];
+  }
 };
+
+__device__ __forceinline__ uint2 lds_row4(const uint16_t *tile, int x, int y) {
+  return *reinterpret_cast<const uint2 *>(tile + tidx(x, y));
+}
 
 // Per-CU geometry + boundary padding, quadrant-relative.
 struct CuPos {
@@ -118,25 +128,24 @@ struct CuPos {
   int padT, padL;  // padding values, intra.cl:102-106, 238-242
 };
 
-__device__ __forceinline__ uint2 lds_row4(const uint16_t *tile, int x, int y) {
-  return *reinterpret_cast<const uint2 *>(tile + tidx(x, y));
-}
-
-__device__ __forceinline__ CuPos cu_pos(const Job &j, int ctu_x, int ctu_y, int qx, int qy, const uint16_t *rt) {
+template <bool LAT>
+__device__ __forceinline__ CuPos cu_pos(const Job &j, int fx0, int fy0, const RefTile<LAT> &rt) {
   CuPos c;
   c.lx = j.lx;
   c.ly = j.ly;
-  c.top = ctu_y + qy + c.ly > 0;
-  c.left = ctu_x + qx + c.lx > 0;
-  c.padT = c.left ? rt[tidx(c.lx - 1, c.ly)] : 512;   // top edge: sample (x-1, 0)
-  c.padL = c.top ? rt[tidx(c.lx, c.ly - 1)] : 512;    // left edge: sample (0, y-1)
+  c.top = fy0 + c.ly > 0;
+  c.left = fx0 + c.lx > 0;
+  c.padT = c.left ? rt.left(c.lx - 1, c.ly) : 512;  // top edge: sample (x-1, 0)
+  c.padL = c.top ? rt.top(c.lx, c.ly - 1) : 512;    // left edge: sample (0, y-1)
   return c;
 }
 
-// Reduced boundaries and MIP input vector of one job, intra.cl:71-73, 127-141, 202-204,
-// 259-279 (box downsampling; a factor of 1 is a copy) and intra.cl:415-454.
-template <int W, int H>
-__device__ __forceinline__ MipIn mip_inputs(const CuPos &c, uint32_t wrow, const uint16_t *rt) {
+// Reduced boundaries (intra.cl:71-73, 127-141, 202-204, 259-279: box downsampling; a
+// factor of 1 is a copy) -> MFMA inputs of both orientations (intra.cl:415-454), as f16
+// in the CU's table entry: input 0 = b0, input k >= 1 = p_k = b_k - b0.  The coefficient
+// tables (mip_kernels.h) fold p_0 and the matrix offset into the accumulator.
+template <int W, int H, bool LAT>
+__device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> &rt, uint8_t *entry) {
   using G = Geo<W, H>;
   constexpr int dfT = W / G::RBS, l2T = ilog2c(dfT), rndT = dfT > 1 ? dfT / 2 : 0;
   constexpr int dfL = H / G::RBS, l2L = ilog2c(dfL), rndL = dfL > 1 ? dfL / 2 : 0;
@@ -147,52 +156,38 @@ __device__ __forceinline__ MipIn mip_inputs(const CuPos &c, uint32_t wrow, const
     if constexpr (dfT >= 4) {
 #pragma unroll
       for (int t = 0; t < dfT; t += 4) {
-        const uint2 v = lds_row4(rt, c.lx + i * dfT + t, c.ly - 1);
+        const uint2 v = rt.top4(c.lx + i * dfT + t, c.ly - 1);
         s += (v.x & 0xffff) + (v.x >> 16) + (v.y & 0xffff) + (v.y >> 16);
       }
     } else {
 #pragma unroll
-      for (int t = 0; t < dfT; t++) s += rt[tidx(c.lx + i * dfT + t, c.ly - 1)];
+      for (int t = 0; t < dfT; t++) s += rt.top(c.lx + i * dfT + t, c.ly - 1);
     }
     redT[i] = c.top ? (s + rndT) >> l2T : c.padT;
     int l = 0;
 #pragma unroll
-    for (int t = 0; t < dfL; t++) l += rt[tidx(c.lx - 1, c.ly + i * dfL + t)];
+    for (int t = 0; t < dfL; t++) l += rt.left(c.lx - 1, c.ly + i * dfL + t);
     redL[i] = c.left ? (l + rndL) >> l2L : c.padL;
   }
-  MipIn m;
-  m.transposed = (wrow & kJobTransposed) != 0;
-  m.wrow = wrow & ~(uint32_t)kJobTransposed;
-  int b[8];
 #pragma unroll
-  for (int i = 0; i < G::RBS; i++) {
-    b[i] = m.transposed ? redL[i] : redT[i];
-    b[G::RBS + i] = m.transposed ? redT[i] : redL[i];
+  for (int o = 0; o < 2; o++) {  // o = 1: transposed modes swap the boundaries (intra.cl:417-418)
+    int b[2 * G::RBS];
+#pragma unroll
+    for (int i = 0; i < G::RBS; i++) {
+      b[i] = o ? redL[i] : redT[i];
+      b[G::RBS + i] = o ? redT[i] : redL[i];
+    }
+    _Float16 hv[8];
+    hv[0] = (_Float16)(short)b[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++) hv[i] = i < 2 * G::RBS ? (_Float16)(short)(b[i < 2 * G::RBS ? i : 0] - b[0]) : (_Float16)0;
+    uint4 v;
+    v.x = __builtin_bit_cast(uint32_t, (h2){hv[0], hv[1]});
+    v.y = __builtin_bit_cast(uint32_t, (h2){hv[2], hv[3]});
+    v.z = __builtin_bit_cast(uint32_t, (h2){hv[4], hv[5]});
+    v.w = __builtin_bit_cast(uint32_t, (h2){hv[6], hv[7]});
+    *reinterpret_cast<uint4 *>(entry + 16 * o) = v;
   }
-#pragma unroll
-  for (int i = 2 * G::RBS; i < 8; i++) b[i] = b[0];
-  m.b0 = b[0];
-  int pv[8], psum = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) pv[i] = b[i] - m.b0;
-  pv[0] = G::SID == 2 ? 0 : 512 - m.b0;  // intra.cl:446
-#pragma unroll
-  for (int i = 0; i < 2 * G::RBS; i++) psum += pv[i];
-  m.offset = 32 - 32 * psum;             // intra.cl:449-454
-#pragma unroll
-  for (int i = 0; i < 4; i++) m.p[i] = s2{(short)pv[2 * i], (short)pv[2 * i + 1]};
-  return m;
-}
-
-// Both modes of a pair at stored reduced position (k, kx); transposed modes store output
-// j at (j % R, j / R), intra.cl:402-406, 485.
-template <int W, int H>
-__device__ __forceinline__ s2 red_direct(const MipIn &m, const int16_t *w, int k, int kx) {
-  using G = Geo<W, H>;
-  const int j = m.transposed ? kx * G::R + k : k * G::R + kx;
-  const int a = gemv<G::SID>(m.p, w + (m.wrow + j) * 8, m.offset, m.b0);
-  const int b = gemv<G::SID>(m.p, w + (m.wrow + G::NOUT + j) * 8, m.offset, m.b0);
-  return s2{(short)a, (short)b};
 }
 
 struct BlockAcc {
@@ -253,14 +248,6 @@ struct Acc {
   }
 };
 
-struct Ctx {
-  const SearchArgs *a;
-  const uint16_t *org, *ref;  // quadrant tiles (distortion / reference samples)
-  const int16_t *w;           // expanded weights (LDS)
-  uint32_t *wave;             // wave-private LDS: job table + reduced-prediction scratch
-  int ctu, frame, ctu_x, ctu_y, qx, qy;  // qx, qy: quadrant origin inside the CTU
-};
-
 // Horizontal pass of anchor row k (CU row k*UV + UV-1) at strip columns x0..x0+3,
 // intra.cl:816-843; the first UH columns interpolate from the left boundary sample.
 // ((UH-o)*before + o*after + UH/2) >> LH == (base + o*delta) >> LH with
@@ -293,15 +280,37 @@ __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, int le
   }
 }
 
-// Walk one strip of one job: prediction rows (upsampling, intra.cl:815-912) streamed
-// through the block transform.  The loops follow the upsampling windows, so every
-// interpolation weight is a compile-time constant (or a wave-uniform loop index).
-template <int W, int H, class RED>
-__device__ __forceinline__ void walk_strip(const Ctx &x, const CuPos &c, const RED &red, int x0, Acc &acc) {
+// Original samples of a lane's strip (rows [y0, y0 + N)): kept in VGPRs across the mode
+// pairs for 4-row CUs, re-read from LDS otherwise (register budget).
+template <int H>
+struct OrigRows {
+  static constexpr bool CACHED = H <= 4;
+  uint2 r[CACHED ? H : 1];
+  const uint16_t *tile;
+  int x, y;
+  __device__ __forceinline__ void load(const uint16_t *t, int xx, int yy) {
+    tile = t;
+    x = xx;
+    y = yy;
+    if constexpr (CACHED) {
+#pragma unroll
+      for (int i = 0; i < H; i++) r[i] = lds_row4(t, xx, yy + i);
+    }
+  }
+  __device__ __forceinline__ uint2 operator()(int i) const {
+    if constexpr (CACHED) return r[i];
+    else return lds_row4(tile, x, y + i);
+  }
+};
+
+// Walk one strip of one CU for one mode pair over upsampling windows [k0, k1) (rows for
+// UV == 1 and 4x4): prediction rows (upsampling, intra.cl:815-912) streamed through the
+// block transform.  `prev` is the anchor row above window k0 (vertical pass state).
+template <int W, int H, bool LAT, class RED>
+__device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &rt, const OrigRows<H> &orig,
+                                           const RED &red, int x0, int k0, int k1, s2 (&prev)[4], Acc &acc) {
   using G = Geo<W, H>;
-  const uint16_t *rt = x.ref, *ot = x.org;
-  auto left_at = [&](int y) { return c.left ? (int)rt[tidx(c.lx - 1, c.ly + y)] : c.padL; };
-  auto orow = [&](int y) { return lds_row4(ot, c.lx + x0, c.ly + y); };
+  auto left_at = [&](int y) { return c.left ? rt.left(c.lx - 1, c.ly + y) : c.padL; };
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
     BlockAcc b;
@@ -310,163 +319,264 @@ __device__ __forceinline__ void walk_strip(const Ctx &x, const CuPos &c, const R
       s2 prow[4];
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) prow[cc] = red(i, cc);
-      block_row(b, i, prow, orow(i));
+      block_row(b, i, prow, orig(i));
     }
     u2 sad, satd;
     block_finish(b, sad, satd);
     acc.add(sad, satd);
   } else if constexpr (G::UV == 1) {
-    // every row is an anchor row (horizontal pass only)
-#pragma unroll 1
-    for (int by = 0; by < H / 4; by++) {
+    // every row is an anchor row (horizontal pass only); [k0, k1) are rows
+    (void)k1;
+#pragma unroll
+    for (int bi = 0; bi < G::KV / 4; bi++) {
+      const int by = k0 / 4 + bi;
       BlockAcc b;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         s2 prow[4];
         anchor_row<W, H>(red, 4 * by + i, x0, left_at(4 * by + i), prow);
-        block_row(b, i, prow, orow(4 * by + i));
+        block_row(b, i, prow, orig(4 * by + i));
+      }
+      u2 sad, satd;
+      block_finish(b, sad, satd);
+      acc.add(sad, satd);
+    }
+  } else if constexpr (G::UV == 2) {
+    // Vertical pass (intra.cl:867-893) with two windows per 4x4 block: the row between
+    // anchors k-1 and k is (prev + next + 1) >> 1.
+    constexpr int kUnroll = H <= 8 ? 2 : 1;
+    constexpr int NBLK = (G::CHUNKED ? 4 : G::KV) / 2;  // blocks in [k0, k1)
+    (void)k1;
+#pragma unroll kUnroll
+    for (int bi = 0; bi < NBLK; bi++) {
+      const int by = k0 / 2 + bi;
+      BlockAcc b;
+#pragma unroll
+      for (int hh = 0; hh < 2; hh++) {
+        const int k = 2 * by + hh;
+        s2 next[4], mid[4];
+        anchor_row<W, H>(red, k, x0, left_at(2 * k + 1), next);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) mid[cc] = as_s2((as_u2(prev[cc]) + as_u2(next[cc]) + (u2){1, 1}) >> (u2){1, 1});
+        block_row(b, 2 * hh, mid, orig(2 * k));
+        block_row(b, 2 * hh + 1, next, orig(2 * k + 1));
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
       }
       u2 sad, satd;
       block_finish(b, sad, satd);
       acc.add(sad, satd);
     }
   } else {
-    // Vertical pass (intra.cl:867-893): row o (1..UV) of window k interpolates between
-    // anchor k-1 (or the top boundary) and anchor k: (base + o*delta) >> LV with
+    // Vertical pass: row o (1..UV) of window k is (base + o*delta) >> LV with
     // base = (prev << LV) + UV/2, the reference numerator, in [0, 8188]; o = UV gives the
     // anchor itself.  16-bit wrap-around in o*delta cancels in the in-range sum.
-    s2 prev[4];
-    {
-      const uint2 tv = lds_row4(rt, c.lx + x0, c.ly - 1);
-      const int t4[4] = {(int)(tv.x & 0xffff), (int)(tv.x >> 16), (int)(tv.y & 0xffff), (int)(tv.y >> 16)};
-#pragma unroll
-      for (int cc = 0; cc < 4; cc++) prev[cc] = splat(c.top ? t4[cc] : c.padT);
-    }
-    if constexpr (G::UV == 2) {
-      // two windows per 4x4 block
+    constexpr int NB = G::UV / 4;  // blocks per window
 #pragma unroll 1
-      for (int by = 0; by < H / 4; by++) {
+    for (int k = k0; k < k1; k++) {
+      s2 next[4];
+      anchor_row<W, H>(red, k, x0, left_at(k * G::UV + G::UV - 1), next);
+      u2 delta[4], base[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; cc++) {
+        delta[cc] = as_u2(next[cc]) - as_u2(prev[cc]);
+        base[cc] = (as_u2(prev[cc]) << (u2){G::LV, G::LV}) + (u2){G::UV / 2, G::UV / 2};
+      }
+#pragma unroll 1
+      for (int bi = 0; bi < NB; bi++) {
         BlockAcc b;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const int k = 2 * by + h;
-          s2 next[4], mid[4];
-          anchor_row<W, H>(red, k, x0, left_at(2 * k + 1), next);
+        for (int i = 0; i < 4; i++) {
+          const unsigned short o = (unsigned short)(4 * bi + i + 1);
+          s2 prow[4];
 #pragma unroll
-          for (int cc = 0; cc < 4; cc++) mid[cc] = as_s2((as_u2(prev[cc]) + as_u2(next[cc]) + (u2){1, 1}) >> (u2){1, 1});
-          block_row(b, 2 * h, mid, orow(2 * k));
-          block_row(b, 2 * h + 1, next, orow(2 * k + 1));
-#pragma unroll
-          for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
+          for (int cc = 0; cc < 4; cc++) prow[cc] = as_s2(((u2){o, o} * delta[cc] + base[cc]) >> (u2){G::LV, G::LV});
+          block_row(b, i, prow, orig(k * G::UV + 4 * bi + i));
         }
         u2 sad, satd;
         block_finish(b, sad, satd);
         acc.add(sad, satd);
       }
+#pragma unroll
+      for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
+    }
+  }
+}
+
+struct Ctx {
+  const SearchArgs *a;
+  const uint16_t *org;        // quadrant tile of original samples
+  const uint16_t *ref;        // reference samples: == org (full tile) or the ALT lattice
+  const uint8_t *w;           // MIP coefficients (LDS): f16 rows, then f32 accumulator rows
+  const uint8_t *zero;        // zero-filled LDS (masked MFMA inputs)
+  uint8_t *wave;              // wave-private LDS: CU table + scratch
+  int ctu, frame;
+  int fx0, fy0;               // quadrant origin in the frame
+};
+
+// Phase A for mode pair q: reduced predictions of every CU of the task,
+//   D[j][n] = C[j] + sum_k A[j][k] B[k][n]     (16x16x16 f16 MFMA, f32 accumulate, exact)
+// rows j = MIP matrix outputs, columns n = (CU 8*cs + n/2, mode 2q + n%2), K = the 8 inputs
+// of mode 2q (k < 8) and of mode 2q+1 (k >= 8), block-diagonal.  floor(D) clipped to
+// [0, 1023] equals the reference's clamp(((offset + sum p*w) >> 6) + b0) (intra.cl:449-482;
+// coefficient restatement in mip_kernels.h).  Results go to scratch[pos][slot] (16-bit
+// halves = modes), pos = stored position (transposed modes store output j at (j%R, j/R),
+// intra.cl:402-406, 485).  CHUNKED classes produce reduced rows [4*chunk, 4*chunk + 4).
+template <int W, int H, bool TR>
+__device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, int chunk) {
+  using G = Geo<W, H>;
+  const int r = lane & 15, h = lane >> 4;
+  const int m0 = TR ? 2 * q - G::MODES : 2 * q;
+  // A: coefficient row of mode m0 + (h >> 1), inputs 4*(h & 1)..+3
+  const int jrow = (G::SID == 2 && TR) ? 8 * (r >> 2) + (r & 3) : r;
+  const uint8_t *abase = x.w + ((G::WBASE + (m0 + (h >> 1)) * G::NOUT + jrow) * 8 + 4 * (h & 1)) * 2;
+  // B: column r = (slot 8*cs + r/2, mode r&1), nonzero only in the K half of its mode
+  const bool bsel = (h >> 1) == (r & 1);
+  const uint8_t *bbase = bsel ? x.wave + (r >> 1) * kEntryBytes + (TR ? 16 : 0) + 8 * (h & 1) : x.zero;
+  // C: per output row (sizeId 1/0), 0.5 for sizeId 2
+  f4 cin;
+  if constexpr (G::SID == 2) {
+    cin = (f4){0.5f, 0.5f, 0.5f, 0.5f};
+  } else {
+    const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1);
+    cin = *reinterpret_cast<const f4 *>(ct + (m0 + (r & 1)) * G::NOUT + 4 * h);
+  }
+  const int ncs = (ncu + 7) >> 3;
+  constexpr int NRB = G::CPOS / 16;  // 16-row blocks in this chunk
+  // the lane's 4 results of block rb sit at stored positions pos0 + i * PSTEP
+  constexpr int PSTEP = G::SID == 2 ? (TR ? 8 : 1) : (TR ? 4 : 1);
+  uint8_t *lane_dst = x.wave + kCuTableBytes + (TR ? h : 4 * h) * G::SLOTS * 4 +
+                      (r >> 1) * 4 + 2 * (r & 1);
+#pragma unroll
+  for (int rb = 0; rb < NRB; rb++) {
+    int jofs, pofs;  // uniform: matrix row offset, stored-position offset of the block
+    if constexpr (G::SID == 2) {
+      const int rbg = G::CHUNKED ? 2 * chunk + rb : rb;  // 16-row block 0..3 of the matrix
+      const int cofs = G::CHUNKED ? 32 * chunk : 0;
+      if constexpr (!TR) {
+        jofs = 16 * rbg;
+        pofs = 16 * rbg - cofs;
+      } else {  // output j = 8*(h + 4*rr) + i + 4*cc -> position (i + 4cc, h + 4rr)
+        const int cc = rbg >> 1, rr = rbg & 1;
+        jofs = 32 * rr + 4 * cc;
+        pofs = 32 * cc + 4 * rr - cofs;
+      }
     } else {
-      constexpr int NB = G::UV / 4;  // blocks per window
+      jofs = 0;
+      pofs = 0;
+    }
+    const h4 av = *reinterpret_cast<const h4 *>(abase + jofs * 16);
 #pragma unroll 1
-      for (int k = 0; k < G::R; k++) {
-        s2 next[4];
-        anchor_row<W, H>(red, k, x0, left_at(k * G::UV + G::UV - 1), next);
-        u2 delta[4], base[4];
+    for (int cs = 0; cs < ncs; cs++) {
+      const h4 bv = *reinterpret_cast<const h4 *>(bbase + cs * 8 * kEntryBytes);
+      const f4 d = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bv, cin, 0, 0, 0);
+      // columns of slots >= ncu hold garbage; they land in unused scratch columns unless
+      // the class has fewer than 8 slots
+      if (G::SLOTS % 8 == 0 || 8 * cs + (r >> 1) < ncu) {
+        uint8_t *dst = lane_dst + (pofs * G::SLOTS + 8 * cs) * 4;
 #pragma unroll
-        for (int cc = 0; cc < 4; cc++) {
-          delta[cc] = as_u2(next[cc]) - as_u2(prev[cc]);
-          base[cc] = (as_u2(prev[cc]) << (u2){G::LV, G::LV}) + (u2){G::UV / 2, G::UV / 2};
+        for (int i = 0; i < 4; i++) {
+          const uint32_t v = (uint32_t)__builtin_amdgcn_fmed3f(d[i], 0.0f, 1023.5f);  // floor + clip
+          *reinterpret_cast<uint16_t *>(dst + i * PSTEP * G::SLOTS * 4) = (uint16_t)v;
         }
-#pragma unroll 2
-        for (int bi = 0; bi < NB; bi++) {
-          BlockAcc b;
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const unsigned short o = (unsigned short)(4 * bi + i + 1);
-            s2 prow[4];
-#pragma unroll
-            for (int cc = 0; cc < 4; cc++) prow[cc] = as_s2(((u2){o, o} * delta[cc] + base[cc]) >> (u2){G::LV, G::LV});
-            block_row(b, i, prow, orow(k * G::UV + 4 * bi + i));
-          }
-          u2 sad, satd;
-          block_finish(b, sad, satd);
-          acc.add(sad, satd);
-        }
-#pragma unroll
-        for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
       }
     }
   }
 }
 
 template <int W, int H>
-__device__ __forceinline__ void run_task(const Ctx &x, const WaveTask &task, int lane) {
+__device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, int chunk) {
+  if (q >= Geo<W, H>::MODES / 2) phase_a<W, H, true>(x, lane, ncu, q, chunk);
+  else phase_a<W, H, false>(x, lane, ncu, q, chunk);
+}
+
+// Opaque copy of a value: keeps per-class lane arithmetic inside its switch case (hoisted
+// out of the task loop it would stay live through every class and spill).
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("; opaque" : "+v"(v));
+  return v;
+}
+
+template <int W, int H, bool LAT>
+__device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, const WaveTask &task, int lane_in) {
   using G = Geo<W, H>;
+  const int lane = opaque(lane_in);
   const SearchArgs &a = *x.a;
-  const int nj = task.njobs;
-  const Job *jobs = a.jobs + task.job0;
-  const int jl = lane / G::S, sx = lane - jl * G::S, x0 = 4 * sx;
-  const bool active = jl < nj;
-  const Job job = jobs[min(jl, nj - 1)];
-  const CuPos c = cu_pos(job, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
-  Acc acc;
+  const int ncu = task.ncu;
+  const Job *jobs = a.jobs + task.cu0;
+  // lane = (slot, row part v, strip sx); lanes of one CU are adjacent
+  const int slot = lane / (G::S * G::V), sub = lane % (G::S * G::V);
+  const int v = sub / G::S, sx = sub % G::S, x0 = 4 * sx;
+  const bool active = slot < ncu;
+  const int cs = min(slot, ncu - 1);
+  const Job job = jobs[cs];
+  const CuPos c = cu_pos(job, x.fx0, x.fy0, rt);
 
-  if constexpr (G::DIRECT) {
-    const MipIn m = mip_inputs<W, H>(c, job.wrow, x.ref);
-    auto red = [&](int k, int kx) { return red_direct<W, H>(m, x.w, k, kx); };
-    walk_strip<W, H>(x, c, red, x0, acc);
-  } else {
-    // ---- phase A: each job's reduced prediction once, into the wave's scratch
-    uint32_t *table = x.wave;
-    uint32_t *scr = x.wave + 64 * kJobWords;
-    constexpr int kStride = G::NOUT + 1;  // +1 dword: different jobs hit different banks
-    if (lane < nj) {
-      const Job jb = jobs[lane];
-      const CuPos cj = cu_pos(jb, x.ctu_x, x.ctu_y, x.qx, x.qy, x.ref);
-      const MipIn m = mip_inputs<W, H>(cj, jb.wrow, x.ref);
-      uint4 *e = reinterpret_cast<uint4 *>(table + lane * kJobWords);
-      e[0] = make_uint4(as_u32(m.p[0]), as_u32(m.p[1]), as_u32(m.p[2]), as_u32(m.p[3]));
-      e[1] = make_uint4((uint32_t)m.offset, (uint32_t)m.b0, (uint32_t)m.wrow, (uint32_t)m.transposed);
-    }
-    wave_lds_sync();
-    const int total = nj * G::NOUT;
-#pragma unroll 1
-    for (int o = lane; o < ((total + 63) & ~63); o += 64) {
-      const int jb = min(o / G::NOUT, nj - 1), j = o % G::NOUT;
-      const uint4 *e = reinterpret_cast<const uint4 *>(table + jb * kJobWords);
-      const uint4 e0 = e[0], e1 = e[1];
-      const s2 p[4] = {as_s2(e0.x), as_s2(e0.y), as_s2(e0.z), as_s2(e0.w)};
-      const int off = (int)e1.x, b0 = (int)e1.y, wrow = (int)e1.z;
-      const int v0 = gemv<G::SID>(p, x.w + (wrow + j) * 8, off, b0);
-      const int v1 = gemv<G::SID>(p, x.w + (wrow + G::NOUT + j) * 8, off, b0);
-      const int pos = e1.w ? (j % G::R) * G::R + j / G::R : j;
-      if (o < total) scr[jb * kStride + pos] = (uint32_t)v0 | ((uint32_t)v1 << 16);
-    }
-    wave_lds_sync();
-    // ---- phase B
-    const uint32_t *mine = scr + min(jl, nj - 1) * kStride;
-    auto red = [&](int k, int kx) { return as_s2(mine[k * G::R + kx]); };
-    walk_strip<W, H>(x, c, red, x0, acc);
-    wave_lds_sync();  // scratch and table are reused by the next task
+  // ---- per-CU MFMA inputs of both orientations -> wave table
+  if (lane < ncu) {
+    const Job jb = jobs[lane];
+    const CuPos cj = cu_pos(jb, x.fx0, x.fy0, rt);
+    write_inputs<W, H>(cj, rt, x.wave + lane * kEntryBytes);
   }
-
-  // ---- combine the strips of one job: adjacent lanes, xor butterfly
+  OrigRows<H> orig;
+  orig.load(x.org, c.lx + x0, c.ly);
+  const bool avail = x.fx0 + c.lx + W <= a.width && x.fy0 + c.ly + H <= a.height;
+  const size_t cbase = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
+  const uint32_t *mine = reinterpret_cast<const uint32_t *>(x.wave + kCuTableBytes) + cs;
+  auto red = [&](int k, int kx) { return as_s2(mine[(k * G::R + kx) * G::SLOTS]); };
+  s2 top[4];  // top boundary of the strip: upsampling state above window 0
+  {
+    const uint2 tv = rt.top4(c.lx + x0, c.ly - 1);
+    const int t4[4] = {(int)(tv.x & 0xffff), (int)(tv.x >> 16), (int)(tv.y & 0xffff), (int)(tv.y >> 16)};
 #pragma unroll
-  for (int off = 1; off < G::S; off <<= 1) {
-    acc.sad0 += __shfl_xor(acc.sad0, off);
-    acc.sad1 += __shfl_xor(acc.sad1, off);
-    acc.satd0 += __shfl_xor(acc.satd0, off);
-    acc.satd1 += __shfl_xor(acc.satd1, off);
+    for (int cc = 0; cc < 4; cc++) top[cc] = splat(c.top ? t4[cc] : c.padT);
   }
-  if (active && sx == 0) {
-    const int fx = x.ctu_x + x.qx + c.lx, fy = x.ctu_y + x.qy + c.ly;
-    const bool avail = fx + W <= a.width && fy + H <= a.height;
-    const size_t idx = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
-    const int c0 = avail ? min(2 * (int)acc.sad0, (int)acc.satd0) : kUnavailable;  // intra.cl:1166
-    const int c1 = avail ? min(2 * (int)acc.sad1, (int)acc.satd1) : kUnavailable;
-    *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
-    if (a.sad)
-      *reinterpret_cast<int2 *>(a.sad + idx) = avail ? make_int2(acc.sad0, acc.sad1) : make_int2(kUnavailable, kUnavailable);
-    if (a.satd)
-      *reinterpret_cast<int2 *>(a.satd + idx) = avail ? make_int2(acc.satd0, acc.satd1) : make_int2(kUnavailable, kUnavailable);
+  wave_lds_sync();
+
+#pragma unroll 1
+  for (int q = task.q0; q < task.q1; q++) {
+    Acc acc;
+    s2 prev[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; cc++) prev[cc] = top[cc];
+    phase_a<W, H>(x, lane, ncu, q, 0);
+    wave_lds_sync();
+    if constexpr (G::CHUNKED) {
+      walk_strip<W, H>(c, rt, orig, red, x0, 0, 4, prev, acc);
+      wave_lds_sync();
+      phase_a<W, H>(x, lane, ncu, q, 1);
+      wave_lds_sync();
+      auto red_hi = [&](int k, int kx) { return as_s2(mine[((k - 4) * G::R + kx) * G::SLOTS]); };
+      walk_strip<W, H>(c, rt, orig, red_hi, x0, 4, 8, prev, acc);  // prev carries anchor row 3
+    } else if constexpr (G::SID == 0) {
+      walk_strip<W, H>(c, rt, orig, red, x0, 0, 4, prev, acc);
+    } else {
+      // row part v: windows [v*KV, (v+1)*KV) (rows when UV == 1)
+      const int k0 = G::V > 1 ? v * G::KV : 0;
+      if constexpr (G::V > 1 && G::UV > 1) {
+        if (k0 > 0) anchor_row<W, H>(red, k0 - 1, x0, c.left ? rt.left(c.lx - 1, c.ly + k0 * G::UV - 1) : c.padL, prev);
+      }
+      walk_strip<W, H>(c, rt, orig, red, x0, k0, k0 + G::KV, prev, acc);
+    }
+    wave_lds_sync();  // the scratch is rewritten by the next pair
+    // ---- combine strips and row parts of one CU: adjacent lanes, xor butterfly
+#pragma unroll
+    for (int off = 1; off < G::S * G::V; off <<= 1) {
+      acc.sad0 += __shfl_xor(acc.sad0, off);
+      acc.sad1 += __shfl_xor(acc.sad1, off);
+      acc.satd0 += __shfl_xor(acc.satd0, off);
+      acc.satd1 += __shfl_xor(acc.satd1, off);
+    }
+    if (active && sub == 0) {
+      const size_t idx = cbase + 2 * q;
+      const int c0 = avail ? min(2 * (int)acc.sad0, (int)acc.satd0) : kUnavailable;  // intra.cl:1166
+      const int c1 = avail ? min(2 * (int)acc.sad1, (int)acc.satd1) : kUnavailable;
+      *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
+      if (a.sad)
+        *reinterpret_cast<int2 *>(a.sad + idx) = avail ? make_int2(acc.sad0, acc.sad1) : make_int2(kUnavailable, kUnavailable);
+      if (a.satd)
+        *reinterpret_cast<int2 *>(a.satd + idx) = avail ? make_int2(acc.satd0, acc.satd1) : make_int2(kUnavailable, kUnavailable);
+    }
   }
 }
 
@@ -486,34 +596,63 @@ __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame,
   }
 }
 
+// Stage the reference lattice (ALT): rows 4i-1 (columns -4..63), columns 4i-1 (rows -1..63).
+__device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
+                                              int x0, int y0) {
+  constexpr int kChunks = kPitch / 4;
+  for (int i = threadIdx.x; i < 16 * kChunks; i += blockDim.x) {
+    const int row = i / kChunks, ch = i - row * kChunks;
+    const int fy = y0 + 4 * row - 1, fx = x0 - kColOff + 4 * ch;
+    uint2 v = make_uint2(0, 0);
+    if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
+      v = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
+    *reinterpret_cast<uint2 *>(dst + row * kLatRowPitch + 4 * ch) = v;
+  }
+  uint16_t *cols = dst + 16 * kLatRowPitch;
+  for (int i = threadIdx.x; i < 16 * 65; i += blockDim.x) {
+    const int col = i / 65, yy = i - col * 65;
+    const int fy = y0 + yy - 1, fx = x0 + 4 * col - 1;
+    cols[col * kLatColPitch + yy] = (fy >= 0 && fy < height && fx >= 0 && fx < width) ? frame[(size_t)fy * width + fx] : 0;
+  }
+}
+
 template <bool ALT>
 __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t *org = smem;
-  uint16_t *ref = ALT ? smem + kTileElems : smem;
-  int16_t *w = reinterpret_cast<int16_t *>(smem + (ALT ? 2 : 1) * kTileElems);
-  uint32_t *waves = reinterpret_cast<uint32_t *>(w + kWeightWords);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint16_t *org = reinterpret_cast<uint16_t *>(smem);
+  uint16_t *ref = ALT ? org + kTileElems : org;
+  uint8_t *w = smem + (kTileElems + (ALT ? kLatElems : 0)) * 2;
+  uint8_t *zero = w + kTableBytes;
+  uint8_t *waves = zero + kZeroBytes;
 
   const int slice = blockIdx.x % a.slices, quad = blockIdx.x / a.slices;
   const int ctu = blockIdx.y, frame = blockIdx.z;
   const int ctu_x = 128 * (ctu % a.ctu_cols), ctu_y = 128 * (ctu / a.ctu_cols);
-  const int qx = 64 * (quad & 1), qy = 64 * (quad >> 1);
+  const int fx0 = ctu_x + 64 * (quad & 1), fy0 = ctu_y + 64 * (quad >> 1);
   const size_t fofs = (size_t)frame * a.width * a.height;
 
-  stage_tile(org, a.orig + fofs, a.width, a.height, ctu_x + qx, ctu_y + qy);
-  if (ALT) stage_tile(ref, a.refs + fofs, a.width, a.height, ctu_x + qx, ctu_y + qy);
-  for (int i = threadIdx.x; i < kWeightWords / 8; i += blockDim.x)
-    reinterpret_cast<uint4 *>(w)[i] = reinterpret_cast<const uint4 *>(a.weights)[i];
+  stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0);
+  if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0);
+  for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x)
+    reinterpret_cast<uint4 *>(w)[i] = a.tables[i];
+  for (int i = threadIdx.x; i < kZeroBytes / 16; i += blockDim.x)
+    reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const Ctx x{&a, org, ref, w, waves + wave * kWaveWords, ctu, frame, ctu_x, ctu_y, qx, qy};
-  const int t0 = a.task_begin[quad], t1 = a.task_begin[quad + 1];
-  for (int t = t0 + slice * kWaves + wave; t < t1; t += kWaves * a.slices) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const Ctx x{&a, org, ref, w, zero, waves + wave * kWaveBytes, ctu, frame, fx0, fy0};
+  const RefTile<ALT> rt{ref};
+  const int list = quad * a.bins + slice * kWaves + wave;
+  const int t1 = a.list_begin[list + 1];
+  for (int t = a.list_begin[list]; t < t1; t++) {
     const WaveTask task = a.tasks[t];
-    switch (c_shape_class[task.shape]) {
-#define MIP_CASE(idx, W, H) \
-  case idx: run_task<W, H>(x, task, lane); break;
+    switch (task.cls) {
+#define MIP_CASE(idx, W, H)                                 \
+  case idx:                                                 \
+    static_assert(size_class(W, H) == idx, "class table");  \
+    if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)        \
+      run_task<W, H, ALT>(x, rt, task, lane);               \
+    break;
       MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
       MIP_CASE(4, 32, 8) MIP_CASE(5, 8, 32) MIP_CASE(6, 16, 16) MIP_CASE(7, 16, 8)
       MIP_CASE(8, 8, 16) MIP_CASE(9, 32, 4) MIP_CASE(10, 4, 32) MIP_CASE(11, 16, 4)
@@ -543,12 +682,14 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
 
 }  // namespace
 
+int search_waves_per_group() { return kWaves; }
+
 size_t search_lds_bytes(bool alt) {
-  return ((alt ? 2 : 1) * kTileElems + kWeightWords) * 2 + (size_t)kWaves * kWaveWords * 4;
+  return (size_t)(kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes + (size_t)kWaves * kWaveBytes;
 }
 
 hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, hipStream_t s) {
-  if (a.slices < 1) return hipErrorInvalidValue;
+  if (a.slices < 1 || a.bins != a.slices * kWaves) return hipErrorInvalidValue;
   const dim3 grid(4 * a.slices, a.nctus, nframes);
   const size_t lds = search_lds_bytes(alt_refs);
   if (alt_refs)

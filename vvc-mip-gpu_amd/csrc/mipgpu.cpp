@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -45,33 +46,50 @@ int axis_pos(int base, int step, int dual, int i) {
   return dual ? base + (i / 2) * step + (i % 2) * dual : base + i * step;
 }
 
-// Expanded weights, layout documented in mip_kernels.h.
-std::vector<int16_t> expand_weights() {
-  std::vector<int16_t> w(mipgpu::kWeightWords, 0);
-  for (int m = 0; m < 6; m++)
-    for (int j = 0; j < 64; j++)
-      for (int i = 0; i < 7; i++) w[(m * 64 + j) * 8 + 1 + i] = kW2[(m * 64 + j) * 7 + i];
-  for (int m = 0; m < 8; m++)
-    for (int j = 0; j < 16; j++)
-      for (int i = 0; i < 8; i++) w[(mipgpu::kWeightRowOffS1 + m * 16 + j) * 8 + i] = kW1[(m * 16 + j) * 8 + i];
-  for (int m = 0; m < 16; m++)
-    for (int j = 0; j < 16; j++)
-      for (int i = 0; i < 4; i++) w[(mipgpu::kWeightRowOffS0 + m * 16 + j) * 8 + i] = kW0[(m * 16 + j) * 4 + i];
-  return w;
+// MIP coefficient tables for the MFMA (layout documented in mip_kernels.h).
+uint16_t to_half(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t u;
+  memcpy(&u, &h, 2);
+  return u;
 }
 
-// Per-quadrant work lists.  Jobs (CU, mode pair) of a shape inside quadrant q are grouped
-// into wave tasks of up to 64/S jobs (S = W/4 strips per CU; at most 16 jobs for shapes
-// that stage reduced predictions in LDS, see mip_search.hip).  Jobs are CU-major for
-// those shapes (lanes of one CU read the same samples) and pair-major for the shapes
-// that compute their matrix products per lane (lanes of a wave share weight rows).
-// Shapes are ordered by rows per strip (descending) so the round-robin assignment of
-// tasks to waves balances, and tasks of one shape stay adjacent.
+std::vector<uint8_t> build_tables() {
+  std::vector<uint8_t> t(mipgpu::kTableBytes, 0);
+  uint16_t *w = reinterpret_cast<uint16_t *>(t.data());
+  float *ctab = reinterpret_cast<float *>(t.data() + mipgpu::kWeightRows * 16);
+  // sizeId 2: reference inputs p_1..p_7 with matrix columns 0..6 (p_0 == 0, mip_matrix.cl:441)
+  for (int m = 0; m < 6; m++)
+    for (int j = 0; j < 64; j++) {
+      uint16_t *row = w + (m * 64 + j) * 8;
+      row[0] = to_half(1.0f);  // (96 - 32) / 64: input 0 carries b0
+      for (int i = 1; i < 8; i++) row[i] = to_half((kW2[(m * 64 + j) * 7 + i - 1] - 32) / 64.0f);
+    }
+  auto small = [&](int base, int modes, int nin, const uint8_t *src) {
+    for (int m = 0; m < modes; m++)
+      for (int j = 0; j < 16; j++) {
+        const uint8_t *wr = src + (m * 16 + j) * nin;
+        uint16_t *row = w + (base + m * 16 + j) * 8;
+        row[0] = to_half((96 - wr[0]) / 64.0f);
+        for (int i = 1; i < nin; i++) row[i] = to_half((wr[i] - 32) / 64.0f);
+        ctab[base - mipgpu::kWeightRowOffS1 + m * 16 + j] = 8.0f * (wr[0] - 32) + 0.5f;
+      }
+  };
+  small(mipgpu::kWeightRowOffS1, 8, 8, kW1);
+  small(mipgpu::kWeightRowOffS0, 16, 4, kW0);
+  return t;
+}
+
+// Per-quadrant work lists.  The CUs of one size class inside quadrant q (several shapes
+// share a class) are split into groups of at most class_slots() CUs; a group and a range
+// of its mode pairs form a wave task.  Tasks are cut so that none exceeds half of a wave's
+// fair share, then assigned to the `bins` task lists of the quadrant longest-first onto
+// the least-loaded list.  Costs are VALU-instruction estimates per lane.
 // MIPGPU_SHAPE_FILTER="i,j,..." (profiling knob) restricts the search to those shapes.
 struct WorkLists {
   std::vector<mipgpu::WaveTask> tasks;
   std::vector<mipgpu::Job> jobs;
-  int task_begin[5];
+  std::vector<int> list_begin;
 };
 
 bool shape_selected(int s) {
@@ -87,51 +105,79 @@ bool shape_selected(int s) {
   return false;
 }
 
-WorkLists build_work() {
-  std::vector<int> order;
-  for (int i = 0; i < MIP_NUM_SHAPES; i++)
-    if (shape_selected(i)) order.push_back(i);
-  std::stable_sort(order.begin(), order.end(), [](int a, int b) { return kShapes[a].h > kShapes[b].h; });
+// Estimated VALU instructions per lane for one mode pair of a task of `ncu` CUs.
+double pair_cost(int cls, int ncu) {
+  const int w = mipgpu::kClassW[cls], h = mipgpu::kClassH[cls];
+  const int sid = mipgpu::class_size_id(w, h), v = mipgpu::class_row_parts(w, h);
+  const int nout = sid == 2 ? 64 : 16;
+  const double blocks = (double)h / 4 / v;
+  const double mfma = ((ncu + 7) / 8) * (nout / 16);
+  return blocks * 200.0 + mfma * 12.0 + 40.0;
+}
+
+WorkLists build_work(int bins) {
   WorkLists wl;
   for (int q = 0; q < 4; q++) {
-    wl.task_begin[q] = (int)wl.tasks.size();
-    for (int s : order) {
+    struct Piece { mipgpu::WaveTask t; double cost; };
+    std::vector<Piece> pieces;
+    std::vector<std::vector<mipgpu::Job>> cls_cus(mipgpu::kNumClasses);
+    for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+      if (!shape_selected(s)) continue;
       const mip_shape_desc &sd = kShapes[s];
-      const int r = sd.size_id == 2 ? 8 : 4;
-      const bool direct = sd.w == r;
-      const int strips = sd.w / 4;
-      // shapes staging reduced predictions: the wave scratch holds 16 x 65 dwords
-      const int per_task = direct ? 64 / strips : std::min(64 / strips, 1040 / (r * r + 1));
-      std::vector<int> cus;
+      const int cls = mipgpu::size_class(sd.w, sd.h);
       for (int cu = 0; cu < sd.ncu; cu++) {
         const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
-        if (x / 64 == (q & 1) && y / 64 == (q >> 1)) cus.push_back(cu);
+        if (x / 64 != (q & 1) || y / 64 != (q >> 1)) continue;
+        cls_cus[cls].push_back(mipgpu::Job{(uint32_t)(sd.cost_offset + cu * 2 * sd.modes), (uint8_t)(x % 64),
+                                           (uint8_t)(y % 64), 0});
       }
-      const int nout = r * r;
-      const int wrow0 = sd.size_id == 2 ? 0 : (sd.size_id == 1 ? mipgpu::kWeightRowOffS1 : mipgpu::kWeightRowOffS0);
-      auto make_job = [&](int cu, int p) {
-        const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
-        const bool tr = 2 * p >= sd.modes;
-        const int mw = tr ? 2 * p - sd.modes : 2 * p;
-        return mipgpu::Job{(uint32_t)(sd.cost_offset + cu * 2 * sd.modes + 2 * p), (uint8_t)(x % 64), (uint8_t)(y % 64),
-                           (uint16_t)((wrow0 + mw * nout) | (tr ? mipgpu::kJobTransposed : 0))};
-      };
-      std::vector<mipgpu::Job> jobs;
-      if (direct) {
-        for (int p = 0; p < sd.modes; p++)
-          for (int cu : cus) jobs.push_back(make_job(cu, p));
-      } else {
-        for (int cu : cus)
-          for (int p = 0; p < sd.modes; p++) jobs.push_back(make_job(cu, p));
+    }
+    double total = 0;
+    for (int cls = 0; cls < mipgpu::kNumClasses; cls++) {
+      const std::vector<mipgpu::Job> &v = cls_cus[cls];
+      if (v.empty()) continue;
+      const int slots = mipgpu::class_slots(mipgpu::kClassW[cls], mipgpu::kClassH[cls]);
+      const int ng = ((int)v.size() + slots - 1) / slots;
+      const int modes = mipgpu::class_size_id(mipgpu::kClassW[cls], mipgpu::kClassH[cls]) == 2 ? 6
+                        : (mipgpu::class_size_id(mipgpu::kClassW[cls], mipgpu::kClassH[cls]) == 1 ? 8 : 16);
+      for (int g = 0, at = 0; g < ng; g++) {  // equal-sized groups
+        const int n = ((int)v.size() - at) / (ng - g);
+        const uint32_t first = (uint32_t)wl.jobs.size();
+        wl.jobs.insert(wl.jobs.end(), v.begin() + at, v.begin() + at + n);
+        at += n;
+        const double c = pair_cost(cls, n);
+        pieces.push_back({mipgpu::WaveTask{(uint8_t)cls, (uint8_t)n, 0, (uint8_t)modes, first}, c});
+        total += c * modes;
       }
-      for (size_t j = 0; j < jobs.size(); j += per_task) {
-        const int n = (int)std::min<size_t>(per_task, jobs.size() - j);
-        wl.tasks.push_back({(uint8_t)s, (uint8_t)n, 0, (uint32_t)(wl.jobs.size() + j)});
+    }
+    // cut long tasks into pair ranges
+    const double cap = total / bins / 2;
+    std::vector<Piece> cut;
+    for (const Piece &p : pieces) {
+      const int np = p.t.q1 - p.t.q0;
+      const int parts = std::max(1, std::min(np, (int)std::ceil(p.cost * np / cap)));
+      for (int i = 0; i < parts; i++) {
+        Piece c = p;
+        c.t.q0 = (uint8_t)(p.t.q0 + np * i / parts);
+        c.t.q1 = (uint8_t)(p.t.q0 + np * (i + 1) / parts);
+        c.cost = p.cost * (c.t.q1 - c.t.q0) + 150.0;
+        cut.push_back(c);
       }
-      wl.jobs.insert(wl.jobs.end(), jobs.begin(), jobs.end());
+    }
+    std::stable_sort(cut.begin(), cut.end(), [](const Piece &a, const Piece &b) { return a.cost > b.cost; });
+    std::vector<double> load(bins, 0.0);
+    std::vector<std::vector<mipgpu::WaveTask>> lists(bins);
+    for (const Piece &p : cut) {
+      const int b = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      load[b] += p.cost;
+      lists[b].push_back(p.t);
+    }
+    for (int b = 0; b < bins; b++) {
+      wl.list_begin.push_back((int)wl.tasks.size());
+      wl.tasks.insert(wl.tasks.end(), lists[b].begin(), lists[b].end());
     }
   }
-  wl.task_begin[4] = (int)wl.tasks.size();
+  wl.list_begin.push_back((int)wl.tasks.size());
   return wl;
 }
 
@@ -153,9 +199,9 @@ struct mip_engine {
   uint8_t *d_best = nullptr;
   mipgpu::WaveTask *d_tasks = nullptr;
   mipgpu::Job *d_jobs = nullptr;
-  int task_begin[5] = {0, 0, 0, 0, 0};
-  int16_t *d_weights = nullptr;
-  int slices = 8;
+  int *d_lists = nullptr;
+  uint8_t *d_tables = nullptr;
+  int slices = 1, bins = 8;
 };
 
 extern "C" {
@@ -206,7 +252,7 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tasks,
-                  (void *)e->d_jobs, (void *)e->d_weights})
+                  (void *)e->d_jobs, (void *)e->d_lists, (void *)e->d_tables})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -257,19 +303,21 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   }
   ALLOC(e->d_best, ncu);
   ALLOC(e->d_best_cost, ncu * 4);
-  const WorkLists wl = build_work();
-  for (int q = 0; q < 5; q++) e->task_begin[q] = wl.task_begin[q];
+  e->slices = o.slices_per_ctu > 0 ? o.slices_per_ctu : 1;
+  e->bins = e->slices * mipgpu::search_waves_per_group();
+  const WorkLists wl = build_work(e->bins);
   ALLOC(e->d_tasks, std::max<size_t>(1, wl.tasks.size()) * sizeof(mipgpu::WaveTask));
   ALLOC(e->d_jobs, std::max<size_t>(1, wl.jobs.size()) * sizeof(mipgpu::Job));
-  const std::vector<int16_t> w = expand_weights();
-  ALLOC(e->d_weights, w.size() * 2);
+  ALLOC(e->d_lists, wl.list_begin.size() * sizeof(int));
+  const std::vector<uint8_t> tab = build_tables();
+  ALLOC(e->d_tables, tab.size());
 #undef ALLOC
   if ((!wl.tasks.empty() &&
        (hipMemcpy(e->d_tasks, wl.tasks.data(), wl.tasks.size() * sizeof(mipgpu::WaveTask), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->d_jobs, wl.jobs.data(), wl.jobs.size() * sizeof(mipgpu::Job), hipMemcpyHostToDevice) != hipSuccess)) ||
-      hipMemcpy(e->d_weights, w.data(), w.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+      hipMemcpy(e->d_lists, wl.list_begin.data(), wl.list_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(e->d_tables, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail("uploading static tables failed"));
-  e->slices = o.slices_per_ctu > 0 ? o.slices_per_ctu : 1;
   *out = e;
   return 0;
 }
@@ -305,13 +353,14 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.satd = d_satd;
   a.tasks = e->d_tasks;
   a.jobs = e->d_jobs;
-  a.weights = e->d_weights;
+  a.list_begin = e->d_lists;
+  a.tables = reinterpret_cast<const uint4 *>(e->d_tables);
   a.width = e->width;
   a.height = e->height;
   a.ctu_cols = e->ctu_cols;
   a.nctus = e->nctus;
-  for (int q = 0; q < 5; q++) a.task_begin[q] = e->task_begin[q];
   a.slices = e->slices;
+  a.bins = e->bins;
   HIP_TRY(mipgpu::launch_search(a, nframes, alt, s));
   if (d_best || d_best_cost) {
     mipgpu::BestArgs b{d_costs, d_best, d_best_cost, nframes * e->nctus * MIP_CUS_PER_CTU};
