@@ -191,17 +191,20 @@ __device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> 
 }
 
 struct BlockAcc {
-  s2 t[16];  // row-transformed residual
-  s2 pos;    // sum of max(d, 0)
+  s2 t[16];      // row-transformed residual
+  uint32_t pos;  // sum of max(d, 0), both modes packed (see block_finish for the bound)
 };
+
+__device__ __forceinline__ uint32_t as_u32(s2 v) { return __builtin_bit_cast(uint32_t, v); }
 
 // One residual row of a 4x4 block: d = orig - pred, positive-part sum, row butterflies.
 __device__ __forceinline__ void block_row(BlockAcc &b, int i, const s2 (&prow)[4], uint2 orow) {
   const s2 o01 = as_s2(orow.x), o23 = as_s2(orow.y);
   const s2 d0 = s2{o01.x, o01.x} - prow[0], d1 = s2{o01.y, o01.y} - prow[1];
   const s2 d2 = s2{o23.x, o23.x} - prow[2], d3 = s2{o23.y, o23.y} - prow[3];
-  const s2 p = smax(d0, splat(0)) + smax(d1, splat(0)) + smax(d2, splat(0)) + smax(d3, splat(0));
-  b.pos = i == 0 ? p : b.pos + p;
+  const uint32_t p0 = as_u32(smax(d0, splat(0))), p1 = as_u32(smax(d1, splat(0)));
+  const uint32_t p2 = as_u32(smax(d2, splat(0))), p3 = as_u32(smax(d3, splat(0)));
+  b.pos = i == 0 ? p0 + p1 + p2 + p3 : b.pos + p0 + p1 + p2 + p3;
   const s2 s0 = d0 + d1, s1 = d0 - d1, s2_ = d2 + d3, s3 = d2 - d3;
   b.t[4 * i + 0] = s0 + s2_;
   b.t[4 * i + 1] = s1 + s3;
@@ -217,8 +220,11 @@ __device__ __forceinline__ void block_row(BlockAcc &b, int i, const s2 (&prow)[4
 // the seven non-DC pair maxima and U = |AC0| + (|DC| >> 2):  satd = T + ((U + 1) >> 1).
 // By Parseval (||c||_2 = 4 ||d||_2) satd <= 32736 and T <= satd, so u16 holds both.
 // SAD = sum |d| = 2 * sum max(d, 0) - DC <= 16368, exact in 16 bits for the same reason.
+// Sums of non-negative packed halves that stay below 2^16 (pos, T) use plain 32-bit adds
+// (v_add3_u32: no carry crosses the halves).
 __device__ __forceinline__ void block_finish(const BlockAcc &b, u2 &sad, u2 &satd) {
-  s2 T = splat(0), dc = splat(0), ac = splat(0);
+  uint32_t T = 0;
+  s2 dc = splat(0), ac = splat(0);
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     const s2 u0 = b.t[c] + b.t[4 + c], u1 = b.t[c] - b.t[4 + c];
@@ -227,14 +233,14 @@ __device__ __forceinline__ void block_finish(const BlockAcc &b, u2 &sad, u2 &sat
       dc = u0 + u2_;
       ac = u0 - u2_;
     } else {
-      T += smax(smax(u0, u2_), splat(0) - smin(u0, u2_));
+      T += as_u32(smax(smax(u0, u2_), splat(0) - smin(u0, u2_)));
     }
-    T += smax(smax(u1, u3), splat(0) - smin(u1, u3));
+    T += as_u32(smax(smax(u1, u3), splat(0) - smin(u1, u3)));
   }
   const s2 adc = smax(dc, splat(0) - dc), aac = smax(ac, splat(0) - ac);
   const u2 U = as_u2(aac) + (as_u2(adc) >> (u2){2, 2});
-  satd = as_u2(T) + ((U + (u2){1, 1}) >> (u2){1, 1});
-  sad = as_u2(b.pos + b.pos - dc);
+  satd = __builtin_bit_cast(u2, T) + ((U + (u2){1, 1}) >> (u2){1, 1});
+  sad = as_u2(as_s2(b.pos << 1) - dc);
 }
 
 // Packed block results -> 32-bit per-mode accumulators.
@@ -490,6 +496,19 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   else phase_a<W, H, false>(x, lane, ncu, q, chunk);
 }
 
+// Sum over aligned groups of N adjacent lanes, delivered to the last lane of each group:
+// shifted adds within 16-lane rows (v_add with row_shr DPP), then row broadcasts.
+template <int N>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
+  if constexpr (N >= 2) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  if constexpr (N >= 4) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  if constexpr (N >= 8) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  if constexpr (N >= 16) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true); // row_shr:8
+  if constexpr (N >= 32) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
+  if constexpr (N >= 64) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
+  return v;
+}
+
 // Opaque copy of a value: keeps per-class lane arithmetic inside its switch case (hoisted
 // out of the task loop it would stay live through every class and spill).
 __device__ __forceinline__ int opaque(int v) {
@@ -559,15 +578,13 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       walk_strip<W, H>(c, rt, orig, red, x0, k0, k0 + G::KV, prev, acc);
     }
     wave_lds_sync();  // the scratch is rewritten by the next pair
-    // ---- combine strips and row parts of one CU: adjacent lanes, xor butterfly
-#pragma unroll
-    for (int off = 1; off < G::S * G::V; off <<= 1) {
-      acc.sad0 += __shfl_xor(acc.sad0, off);
-      acc.sad1 += __shfl_xor(acc.sad1, off);
-      acc.satd0 += __shfl_xor(acc.satd0, off);
-      acc.satd1 += __shfl_xor(acc.satd1, off);
-    }
-    if (active && sub == 0) {
+    // ---- combine strips and row parts of one CU (adjacent lanes) into its last lane
+    constexpr int GS = G::S * G::V;
+    acc.sad0 = group_sum<GS>(acc.sad0);
+    acc.sad1 = group_sum<GS>(acc.sad1);
+    acc.satd0 = group_sum<GS>(acc.satd0);
+    acc.satd1 = group_sum<GS>(acc.satd1);
+    if (active && sub == GS - 1) {
       const size_t idx = cbase + 2 * q;
       const int c0 = avail ? min(2 * (int)acc.sad0, (int)acc.satd0) : kUnavailable;  // intra.cl:1166
       const int c1 = avail ? min(2 * (int)acc.sad1, (int)acc.satd1) : kUnavailable;
