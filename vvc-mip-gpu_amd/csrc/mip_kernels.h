@@ -37,7 +37,7 @@ constexpr int class_size_id(int w, int h) { return (w == 4 && h == 4) ? 0 : ((w 
 // so that a task still fills the wave.
 constexpr int class_row_parts(int w, int h) {
   return (w == 64 || (w == 16 && h >= 16)) ? 4
-         : ((w == 32 && h >= 8) || (w == 4 && h >= 16) || (w == 16 && h == 8)) ? 2 : 1;
+         : ((w == 32 && h >= 8) || (w == 4 && h >= 16)) ? 2 : 1;
 }
 constexpr int class_slots(int w, int h) { return 64 / ((w / 4) * class_row_parts(w, h)); }
 
@@ -57,12 +57,21 @@ struct SearchArgs {
   int bins;               // task lists per quadrant (= slices * waves per workgroup)
 };
 
-// MIP matrices, restated for an exact f16 MFMA (mip_search.hip, phase A):
+// MIP matrices, restated for an exact f16 MFMA (mip_search.hip, phase A).  The reference
+// computes pred_j = clamp(((32 - 32*sum_k p_k + sum_k p_k*w_jk) >> 6) + b0, 0, 1023) with
+// p_k = b_k - b0 (p_0 = 0 for sizeId 2, 512 - b0 otherwise; intra.cl:415-482).  With
+// w'_k = (w_jk - 32)/64 and a0 = 1 (sizeId 2; its matrix has no column for input 0) or
+// (96 - w_j0)/64 (sizeId 1/0: p_0 = 512 - b0 folded), that is
+//     pred_j = clamp(floor(C_j + a0*b0 + sum_{k>=1} w'_k (b_k - b0)))
+// with C_j = 0.5 (sizeId 2) or 8*(w_j0 - 32) + 0.5.  The MFMA is fed x_k = 1024 + b_k (f16
+// bit pattern 0x6400 | b_k, no conversion), so the stored coefficients are
+//     A_j0 = a0 - sum_{k>=1} w'_k,   A_jk = w'_k (k >= 1),   C'_j = C_j - 1024 * sum_k A_jk.
+// All values are multiples of 1/64 below 2^5 (f16-exact); every partial sum stays below
+// 2^18 in units of 1/64, so the f32 accumulation is exact.
 //   f16 rows [768][8], row = base(sizeId) + mode*R*R + j, base = 0 / 384 / 512 for sizeId
-//   2 / 1 / 0.  Half k is the coefficient of input k: input 0 carries b0 with (96 - w0)/64,
-//   inputs k >= 1 carry p_k with (w_k - 32)/64 (sizeId 2 uses the shifted columns
-//   (w0 := 32, w_1..7 = mip_matrix.cl:441 columns 0..6); sizeId 0 has 4 inputs).
-//   f32 rows [384] (sizeId 1 and 0, from row 384): accumulator init 8*(w0 - 32) + 0.5.
+//   2 / 1 / 0 (sizeId 0: 4 inputs, halves 4..7 zero).
+//   f32 rows [384] (sizeId 1 and 0, from row 384): C'_j.  sizeId 2: C' = 0.5 - 1024 for all j.
+constexpr float kAccInitS2 = 0.5f - 1024.0f;
 constexpr int kWeightRows = 768, kWeightRowOffS1 = 384, kWeightRowOffS0 = 512;
 constexpr int kCtabRows = 384;
 constexpr int kTableBytes = kWeightRows * 16 + kCtabRows * 4;

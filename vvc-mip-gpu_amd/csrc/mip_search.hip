@@ -53,11 +53,11 @@ constexpr int kTileElems = (65 * kPitch + 7) / 8 * 8;  // quadrant rows -1..63
 constexpr int kLatRowPitch = kPitch, kLatColPitch = 66;
 constexpr int kLatElems = (16 * kLatRowPitch + 16 * kLatColPitch + 7) / 8 * 8;
 // Wave-private LDS: per-CU MFMA inputs + reduced-prediction scratch.
-constexpr int kEntryBytes = 32;                         // 2 orientations x 8 f16 inputs
+constexpr int kEntryBytes = 16;                         // 8 f16 MFMA inputs per CU
 constexpr int kCuTableBytes = 64 * kEntryBytes;
 constexpr int kScratchWords = 1024;                     // [position][slot] packed mode pairs
 constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
-constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 32;    // > every uniform B offset + 8 B
+constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 16;    // > every uniform B offset + 8 B
 constexpr int kUnavailable = 0x7fffffff;
 
 __device__ __forceinline__ int tidx(int x, int y) { return (y + 1) * kPitch + x + kColOff; }
@@ -141,18 +141,20 @@ __device__ __forceinline__ CuPos cu_pos(const Job &j, int fx0, int fy0, const Re
 }
 
 // Reduced boundaries (intra.cl:71-73, 127-141, 202-204, 259-279: box downsampling; a
-// factor of 1 is a copy) -> MFMA inputs of both orientations (intra.cl:415-454), as f16
-// in the CU's table entry: input 0 = b0, input k >= 1 = p_k = b_k - b0.  The coefficient
-// tables (mip_kernels.h) fold p_0 and the matrix offset into the accumulator.
+// factor of 1 is a copy) -> the CU's MFMA input entry: f16 values 1024 + b for the
+// boundary vector b = (redT, redL) (f16 bit pattern 0x6400 | b, exact for b < 1024).  The
+// transposed orientation (redL, redT) (intra.cl:417-418) is the same entry read with its
+// two 8-byte halves swapped; sizeId 0 stores (T0 T1 L0 L1 | L0 L1 T0 T1) for that.
+// The coefficient tables (mip_kernels.h) absorb p = b - b0, p_0 and the bias.
 template <int W, int H, bool LAT>
 __device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> &rt, uint8_t *entry) {
   using G = Geo<W, H>;
   constexpr int dfT = W / G::RBS, l2T = ilog2c(dfT), rndT = dfT > 1 ? dfT / 2 : 0;
   constexpr int dfL = H / G::RBS, l2L = ilog2c(dfL), rndL = dfL > 1 ? dfL / 2 : 0;
-  int redT[G::RBS], redL[G::RBS];
+  uint32_t redT[G::RBS], redL[G::RBS];
 #pragma unroll
   for (int i = 0; i < G::RBS; i++) {
-    int s = 0;
+    uint32_t s = 0;
     if constexpr (dfT >= 4) {
 #pragma unroll
       for (int t = 0; t < dfT; t += 4) {
@@ -164,30 +166,24 @@ __device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> 
       for (int t = 0; t < dfT; t++) s += rt.top(c.lx + i * dfT + t, c.ly - 1);
     }
     redT[i] = c.top ? (s + rndT) >> l2T : c.padT;
-    int l = 0;
+    uint32_t l = 0;
 #pragma unroll
     for (int t = 0; t < dfL; t++) l += rt.left(c.lx - 1, c.ly + i * dfL + t);
     redL[i] = c.left ? (l + rndL) >> l2L : c.padL;
   }
-#pragma unroll
-  for (int o = 0; o < 2; o++) {  // o = 1: transposed modes swap the boundaries (intra.cl:417-418)
-    int b[2 * G::RBS];
-#pragma unroll
-    for (int i = 0; i < G::RBS; i++) {
-      b[i] = o ? redL[i] : redT[i];
-      b[G::RBS + i] = o ? redT[i] : redL[i];
-    }
-    _Float16 hv[8];
-    hv[0] = (_Float16)(short)b[0];
-#pragma unroll
-    for (int i = 1; i < 8; i++) hv[i] = i < 2 * G::RBS ? (_Float16)(short)(b[i < 2 * G::RBS ? i : 0] - b[0]) : (_Float16)0;
-    uint4 v;
-    v.x = __builtin_bit_cast(uint32_t, (h2){hv[0], hv[1]});
-    v.y = __builtin_bit_cast(uint32_t, (h2){hv[2], hv[3]});
-    v.z = __builtin_bit_cast(uint32_t, (h2){hv[4], hv[5]});
-    v.w = __builtin_bit_cast(uint32_t, (h2){hv[6], hv[7]});
-    *reinterpret_cast<uint4 *>(entry + 16 * o) = v;
+  constexpr uint32_t kBias = 0x64006400u;  // f16 1024.0 in both halves
+  uint4 e;
+  if constexpr (G::RBS == 4) {
+    e = make_uint4(redT[0] | redT[1] << 16, redT[2] | redT[3] << 16, redL[0] | redL[1] << 16, redL[2] | redL[3] << 16);
+  } else {
+    const uint32_t t01 = redT[0] | redT[1] << 16, l01 = redL[0] | redL[1] << 16;
+    e = make_uint4(t01, l01, l01, t01);
   }
+  e.x |= kBias;
+  e.y |= kBias;
+  e.z |= kBias;
+  e.w |= kBias;
+  *reinterpret_cast<uint4 *>(entry) = e;
 }
 
 struct BlockAcc {
@@ -438,11 +434,11 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   const uint8_t *abase = x.w + ((G::WBASE + (m0 + (h >> 1)) * G::NOUT + jrow) * 8 + 4 * (h & 1)) * 2;
   // B: column r = (slot 8*cs + r/2, mode r&1), nonzero only in the K half of its mode
   const bool bsel = (h >> 1) == (r & 1);
-  const uint8_t *bbase = bsel ? x.wave + (r >> 1) * kEntryBytes + (TR ? 16 : 0) + 8 * (h & 1) : x.zero;
-  // C: per output row (sizeId 1/0), 0.5 for sizeId 2
+  const uint8_t *bbase = bsel ? x.wave + (r >> 1) * kEntryBytes + 8 * ((h & 1) ^ (TR ? 1 : 0)) : x.zero;
+  // C: per output row (sizeId 1/0), a constant for sizeId 2 (mip_kernels.h)
   f4 cin;
   if constexpr (G::SID == 2) {
-    cin = (f4){0.5f, 0.5f, 0.5f, 0.5f};
+    cin = (f4){kAccInitS2, kAccInitS2, kAccInitS2, kAccInitS2};
   } else {
     const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1);
     cin = *reinterpret_cast<const f4 *>(ct + (m0 + (r & 1)) * G::NOUT + 4 * h);

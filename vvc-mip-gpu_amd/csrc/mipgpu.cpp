@@ -58,21 +58,34 @@ std::vector<uint8_t> build_tables() {
   std::vector<uint8_t> t(mipgpu::kTableBytes, 0);
   uint16_t *w = reinterpret_cast<uint16_t *>(t.data());
   float *ctab = reinterpret_cast<float *>(t.data() + mipgpu::kWeightRows * 16);
-  // sizeId 2: reference inputs p_1..p_7 with matrix columns 0..6 (p_0 == 0, mip_matrix.cl:441)
+  // one matrix row: a0 and w'_1..w'_{nin-1} -> A_j (see mip_kernels.h); returns sum_k A_jk
+  auto put = [&](int row, double a0, const double *wp, int nin) {
+    double sum_w = 0, sum_a = 0;
+    for (int k = 1; k < nin; k++) sum_w += wp[k];
+    double a[8] = {a0 - sum_w, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 1; k < nin; k++) a[k] = wp[k];
+    for (int k = 0; k < 8; k++) {
+      w[row * 8 + k] = to_half((float)a[k]);
+      sum_a += a[k];
+    }
+    return sum_a;
+  };
+  // sizeId 2: inputs 1..7 use matrix columns 0..6 (p_0 == 0, mip_matrix.cl:441, intra.cl:459-463)
   for (int m = 0; m < 6; m++)
     for (int j = 0; j < 64; j++) {
-      uint16_t *row = w + (m * 64 + j) * 8;
-      row[0] = to_half(1.0f);  // (96 - 32) / 64: input 0 carries b0
-      for (int i = 1; i < 8; i++) row[i] = to_half((kW2[(m * 64 + j) * 7 + i - 1] - 32) / 64.0f);
+      double wp[8] = {0};
+      for (int k = 1; k < 8; k++) wp[k] = (kW2[(m * 64 + j) * 7 + k - 1] - 32) / 64.0;
+      const double sa = put(m * 64 + j, 1.0, wp, 8);
+      (void)sa;  // == 1: C' is the constant kAccInitS2
     }
   auto small = [&](int base, int modes, int nin, const uint8_t *src) {
     for (int m = 0; m < modes; m++)
       for (int j = 0; j < 16; j++) {
         const uint8_t *wr = src + (m * 16 + j) * nin;
-        uint16_t *row = w + (base + m * 16 + j) * 8;
-        row[0] = to_half((96 - wr[0]) / 64.0f);
-        for (int i = 1; i < nin; i++) row[i] = to_half((wr[i] - 32) / 64.0f);
-        ctab[base - mipgpu::kWeightRowOffS1 + m * 16 + j] = 8.0f * (wr[0] - 32) + 0.5f;
+        double wp[8] = {0};
+        for (int k = 1; k < nin; k++) wp[k] = (wr[k] - 32) / 64.0;
+        const double sa = put(base + m * 16 + j, (96 - wr[0]) / 64.0, wp, nin);
+        ctab[base - mipgpu::kWeightRowOffS1 + m * 16 + j] = (float)(8.0 * (wr[0] - 32) + 0.5 - 1024.0 * sa);
       }
   };
   small(mipgpu::kWeightRowOffS1, 8, 8, kW1);
@@ -103,6 +116,12 @@ bool shape_selected(int s) {
     p = *end ? end + 1 : end;
   }
   return false;
+}
+
+// Task size cap = a wave's fair share / cut_factor (MIPGPU_CUT_FACTOR, tuning knob).
+double cut_factor() {
+  const char *e = getenv("MIPGPU_CUT_FACTOR");
+  return e && atof(e) > 0 ? atof(e) : 2.0;
 }
 
 // Estimated VALU instructions per lane for one mode pair of a task of `ncu` CUs.
@@ -151,7 +170,7 @@ WorkLists build_work(int bins) {
       }
     }
     // cut long tasks into pair ranges
-    const double cap = total / bins / 2;
+    const double cap = total / bins / cut_factor();
     std::vector<Piece> cut;
     for (const Piece &p : pieces) {
       const int np = p.t.q1 - p.t.q0;
