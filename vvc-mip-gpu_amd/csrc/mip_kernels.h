@@ -70,10 +70,11 @@ struct SearchArgs {
 // 2^18 in units of 1/64, so the f32 accumulation is exact.
 //   f16 rows [768][8], row = base(sizeId) + mode*R*R + j, base = 0 / 384 / 512 for sizeId
 //   2 / 1 / 0 (sizeId 0: 4 inputs, halves 4..7 zero).
-//   f32 rows [384] (sizeId 1 and 0, from row 384): C'_j.  sizeId 2: C' = 0.5 - 1024 for all j.
+//   f32 rows [388] (sizeId 1 and 0, from row 384): C'_j; then 4 x kAccInitS2, the sizeId 2
+//   C' = 0.5 - 1024 of every row (read from LDS so it stays in registers).
 constexpr float kAccInitS2 = 0.5f - 1024.0f;
 constexpr int kWeightRows = 768, kWeightRowOffS1 = 384, kWeightRowOffS0 = 512;
-constexpr int kCtabRows = 384;
+constexpr int kCtabRows = 384 + 4;  // + 4 copies of kAccInitS2 (row 384..387)
 constexpr int kTableBytes = kWeightRows * 16 + kCtabRows * 4;
 
 struct BestArgs {

@@ -438,7 +438,7 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   // C: per output row (sizeId 1/0), a constant for sizeId 2 (mip_kernels.h)
   f4 cin;
   if constexpr (G::SID == 2) {
-    cin = (f4){kAccInitS2, kAccInitS2, kAccInitS2, kAccInitS2};
+    cin = *reinterpret_cast<const f4 *>(reinterpret_cast<const float *>(x.w + kWeightRows * 16) + 384);
   } else {
     const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1);
     cin = *reinterpret_cast<const f4 *>(ct + (m0 + (r & 1)) * G::NOUT + 4 * h);

@@ -90,6 +90,7 @@ std::vector<uint8_t> build_tables() {
   };
   small(mipgpu::kWeightRowOffS1, 8, 8, kW1);
   small(mipgpu::kWeightRowOffS0, 16, 4, kW0);
+  for (int i = 0; i < 4; i++) ctab[384 + i] = mipgpu::kAccInitS2;
   return t;
 }
 
