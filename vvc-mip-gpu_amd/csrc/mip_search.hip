@@ -382,9 +382,9 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) {
         delta[cc] = as_u2(next[cc]) - as_u2(prev[cc]);
-        base[cc] = (as_u2(prev[cc]) << (u2){G::LV, G::LV}) + (u2){G::UV / 2, G::UV / 2};
+        base[cc] = as_u2(prev[cc]) * (u2){G::UV, G::UV} + (u2){G::UV / 2, G::UV / 2};
       }
-#pragma unroll 1
+#pragma unroll
       for (int bi = 0; bi < NB; bi++) {
         BlockAcc b;
 #pragma unroll
@@ -392,7 +392,8 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
           const unsigned short o = (unsigned short)(4 * bi + i + 1);
           s2 prow[4];
 #pragma unroll
-          for (int cc = 0; cc < 4; cc++) prow[cc] = as_s2(((u2){o, o} * delta[cc] + base[cc]) >> (u2){G::LV, G::LV});
+          for (int cc = 0; cc < 4; cc++)
+            prow[cc] = o == G::UV ? next[cc] : as_s2(((u2){o, o} * delta[cc] + base[cc]) >> (u2){G::LV, G::LV});
           block_row(b, i, prow, orig(k * G::UV + 4 * bi + i));
         }
         u2 sad, satd;
@@ -443,8 +444,8 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
     const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1);
     cin = *reinterpret_cast<const f4 *>(ct + (m0 + (r & 1)) * G::NOUT + 4 * h);
   }
-  const int ncs = (ncu + 7) >> 3;
-  constexpr int NRB = G::CPOS / 16;  // 16-row blocks in this chunk
+  constexpr int NCS = (G::SLOTS + 7) / 8;  // column sets (8 CUs x 2 modes) of a full task
+  constexpr int NRB = G::CPOS / 16;        // 16-row blocks in this chunk
   // the lane's 4 results of block rb sit at stored positions pos0 + i * PSTEP
   constexpr int PSTEP = G::SID == 2 ? (TR ? 8 : 1) : (TR ? 4 : 1);
   uint8_t *lane_dst = x.wave + kCuTableBytes + (TR ? h : 4 * h) * G::SLOTS * 4 +
@@ -468,8 +469,9 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
       pofs = 0;
     }
     const h4 av = *reinterpret_cast<const h4 *>(abase + jofs * 16);
-#pragma unroll 1
-    for (int cs = 0; cs < ncs; cs++) {
+#pragma unroll
+    for (int cs = 0; cs < NCS; cs++) {
+      if (cs > 0 && 8 * cs >= ncu) break;  // wave-uniform: partial last task
       const h4 bv = *reinterpret_cast<const h4 *>(bbase + cs * 8 * kEntryBytes);
       const f4 d = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bv, cin, 0, 0, 0);
       // columns of slots >= ncu hold garbage; they land in unused scratch columns unless
