@@ -49,13 +49,15 @@ struct SearchArgs {
   int32_t *satd;          // optional, same layout
   const WaveTask *tasks;  // per (quadrant, wave) task lists, concatenated
   const Job *jobs;
-  const int *list_begin;  // task list of (quadrant q, bin b): [list_begin[q*bins+b], list_begin[q*bins+b+1])
+  const int *list_begin;  // task list of (quadrant q, slice s): [list_begin[q*slices+s], list_begin[q*slices+s+1])
   const uint4 *tables;    // kTableBytes: MIP matrices for the MFMA, see below
   int width, height;
   int ctu_cols, nctus;
-  int slices;             // workgroups per CTU quadrant
-  int bins;               // task lists per quadrant (= slices * waves per workgroup)
+  int slices;             // workgroups (task lists) per CTU quadrant
+  uint64_t *wave_clock;   // profiling (MIPGPU_WAVE_TIMING): [workgroup][kClockSlots] cycles per
+                          // task of the workgroup's list; else null
 };
+constexpr int kClockSlots = 128;
 
 // MIP matrices, restated for an exact f16 MFMA (mip_search.hip, phase A).  The reference
 // computes pred_j = clamp(((32 - 32*sum_k p_k + sum_k p_k*w_jk) >> 6) + b0, 0, 1023) with

@@ -55,7 +55,7 @@ constexpr int kLatElems = (16 * kLatRowPitch + 16 * kLatColPitch + 7) / 8 * 8;
 // Wave-private LDS: per-CU MFMA inputs + reduced-prediction scratch.
 constexpr int kEntryBytes = 16;                         // 8 f16 MFMA inputs per CU
 constexpr int kCuTableBytes = 64 * kEntryBytes;
-constexpr int kScratchWords = 1024;                     // [position][slot] packed mode pairs
+constexpr int kScratchWords = 1280;                     // [slot][position] packed mode pairs
 constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
 constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 16;    // > every uniform B offset + 8 B
 constexpr int kUnavailable = 0x7fffffff;
@@ -92,10 +92,12 @@ struct Geo {
   static constexpr int KV = R / V;                    // upsampling windows per row part
   static constexpr bool CHUNKED = SID == 2 && UH == 1;  // 8xH: reduced rows in two halves
   static constexpr int CPOS = CHUNKED ? 32 : NOUT;    // scratch positions per chunk
+  // scratch: [slot][PITCH] dwords; UH == 1 classes read 4 consecutive positions (16-B aligned)
+  static constexpr int PITCH = UH == 1 ? CPOS + 4 : CPOS + 1;
   static constexpr int WBASE = SID == 2 ? 0 : (SID == 1 ? kWeightRowOffS1 : kWeightRowOffS0);
   static constexpr int MODES = SID == 2 ? 6 : (SID == 1 ? 8 : 16);
   static_assert(SLOTS * S * V == 64, "lanes");
-  static_assert(CPOS * SLOTS <= kScratchWords, "scratch");
+  static_assert(SLOTS * PITCH <= kScratchWords, "scratch");
   // a row part is whole upsampling windows and whole 4x4 blocks
   static_assert(V == 1 || (!CHUNKED && SID != 0 && (UV >= 4 || KV % (4 / UV) == 0)), "row parts");
 };
@@ -250,6 +252,23 @@ struct Acc {
   }
 };
 
+// Reduced prediction of the lane's CU in the wave scratch: both modes of the pair per dword,
+// stored position (k, kx) at k*R + kx (rows offset by `k0` for the second half of a chunked
+// class).
+template <int R>
+struct Red {
+  const uint32_t *p;
+  int k0;
+  __device__ __forceinline__ s2 operator()(int k, int kx) const { return as_s2(p[(k + k0) * R + kx]); }
+  __device__ __forceinline__ void row4(int k, int kx, s2 (&out)[4]) const {  // kx % 4 == 0
+    const uint4 v = *reinterpret_cast<const uint4 *>(p + (k + k0) * R + kx);
+    out[0] = as_s2(v.x);
+    out[1] = as_s2(v.y);
+    out[2] = as_s2(v.z);
+    out[3] = as_s2(v.w);
+  }
+};
+
 // Horizontal pass of anchor row k (CU row k*UV + UV-1) at strip columns x0..x0+3,
 // intra.cl:816-843; the first UH columns interpolate from the left boundary sample.
 // ((UH-o)*before + o*after + UH/2) >> LH == (base + o*delta) >> LH with
@@ -258,8 +277,7 @@ template <int W, int H, class RED>
 __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, int left_k, s2 (&a)[4]) {
   using G = Geo<W, H>;
   if constexpr (G::UH == 1) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) a[c] = red(k, x0 + c);
+    red.row4(k, x0, a);
   } else if constexpr (G::UH == 2) {
     const int kx = x0 >> 1;  // covers kx, kx+1
     const s2 r0 = red(k, kx), r1 = red(k, kx + 1);
@@ -319,8 +337,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       s2 prow[4];
-#pragma unroll
-      for (int cc = 0; cc < 4; cc++) prow[cc] = red(i, cc);
+      red.row4(i, 0, prow);
       block_row(b, i, prow, orig(i));
     }
     u2 sad, satd;
@@ -448,8 +465,7 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   constexpr int NRB = G::CPOS / 16;        // 16-row blocks in this chunk
   // the lane's 4 results of block rb sit at stored positions pos0 + i * PSTEP
   constexpr int PSTEP = G::SID == 2 ? (TR ? 8 : 1) : (TR ? 4 : 1);
-  uint8_t *lane_dst = x.wave + kCuTableBytes + (TR ? h : 4 * h) * G::SLOTS * 4 +
-                      (r >> 1) * 4 + 2 * (r & 1);
+  uint8_t *lane_dst = x.wave + kCuTableBytes + ((r >> 1) * G::PITCH + (TR ? h : 4 * h)) * 4 + 2 * (r & 1);
 #pragma unroll
   for (int rb = 0; rb < NRB; rb++) {
     int jofs, pofs;  // uniform: matrix row offset, stored-position offset of the block
@@ -477,11 +493,11 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
       // columns of slots >= ncu hold garbage; they land in unused scratch columns unless
       // the class has fewer than 8 slots
       if (G::SLOTS % 8 == 0 || 8 * cs + (r >> 1) < ncu) {
-        uint8_t *dst = lane_dst + (pofs * G::SLOTS + 8 * cs) * 4;
+        uint8_t *dst = lane_dst + (pofs + 8 * cs * G::PITCH) * 4;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const uint32_t v = (uint32_t)__builtin_amdgcn_fmed3f(d[i], 0.0f, 1023.5f);  // floor + clip
-          *reinterpret_cast<uint16_t *>(dst + i * PSTEP * G::SLOTS * 4) = (uint16_t)v;
+          *reinterpret_cast<uint16_t *>(dst + i * PSTEP * 4) = (uint16_t)v;
         }
       }
     }
@@ -539,8 +555,8 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   orig.load(x.org, c.lx + x0, c.ly);
   const bool avail = x.fx0 + c.lx + W <= a.width && x.fy0 + c.ly + H <= a.height;
   const size_t cbase = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
-  const uint32_t *mine = reinterpret_cast<const uint32_t *>(x.wave + kCuTableBytes) + cs;
-  auto red = [&](int k, int kx) { return as_s2(mine[(k * G::R + kx) * G::SLOTS]); };
+  const uint32_t *mine = reinterpret_cast<const uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
+  const Red<G::R> red{mine, 0};
   s2 top[4];  // top boundary of the strip: upsampling state above window 0
   {
     const uint2 tv = rt.top4(c.lx + x0, c.ly - 1);
@@ -563,7 +579,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       wave_lds_sync();
       phase_a<W, H>(x, lane, ncu, q, 1);
       wave_lds_sync();
-      auto red_hi = [&](int k, int kx) { return as_s2(mine[((k - 4) * G::R + kx) * G::SLOTS]); };
+      const Red<G::R> red_hi{mine, -4};  // chunk 1 holds reduced rows 4..7
       walk_strip<W, H>(c, rt, orig, red_hi, x0, 4, 8, prev, acc);  // prev carries anchor row 3
     } else if constexpr (G::SID == 0) {
       walk_strip<W, H>(c, rt, orig, red, x0, 0, 4, prev, acc);
@@ -652,15 +668,26 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     reinterpret_cast<uint4 *>(w)[i] = a.tables[i];
   for (int i = threadIdx.x; i < kZeroBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
+  uint32_t *next_task = reinterpret_cast<uint32_t *>(waves + kWaves * kWaveBytes);
+  if (threadIdx.x == 0) *next_task = 0;
   __syncthreads();
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const Ctx x{&a, org, ref, w, zero, waves + wave * kWaveBytes, ctu, frame, fx0, fy0};
   const RefTile<ALT> rt{ref};
-  const int list = quad * a.bins + slice * kWaves + wave;
-  const int t1 = a.list_begin[list + 1];
-  for (int t = a.list_begin[list]; t < t1; t++) {
-    const WaveTask task = a.tasks[t];
+  // Waves take the workgroup's tasks (longest first) from an LDS counter, so early
+  // finishers pick up the slack of waves the SIMD arbiter serves later.
+  const int list = quad * a.slices + slice;
+  const int tbase = a.list_begin[list], ntasks = a.list_begin[list + 1] - tbase;
+  uint64_t *clk = a.wave_clock ? a.wave_clock + (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) *
+                                      kClockSlots : nullptr;
+  for (;;) {
+    uint32_t tn = 0;
+    if (lane == 0) tn = atomicAdd(next_task, 1u);
+    const int t = (int)__builtin_amdgcn_readfirstlane(tn);
+    if (t >= ntasks) break;
+    const uint64_t c0 = clk ? __builtin_readcyclecounter() : 0;
+    const WaveTask task = a.tasks[tbase + t];
     switch (task.cls) {
 #define MIP_CASE(idx, W, H)                                 \
   case idx:                                                 \
@@ -676,6 +703,7 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
 #undef MIP_CASE
       default: break;
     }
+    if (clk && lane == 0 && t < kClockSlots) clk[t] = __builtin_readcyclecounter() - c0;
   }
 }
 
@@ -700,11 +728,11 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
 int search_waves_per_group() { return kWaves; }
 
 size_t search_lds_bytes(bool alt) {
-  return (size_t)(kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes + (size_t)kWaves * kWaveBytes;
+  return (size_t)(kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes + (size_t)kWaves * kWaveBytes + 16;
 }
 
 hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, hipStream_t s) {
-  if (a.slices < 1 || a.bins != a.slices * kWaves) return hipErrorInvalidValue;
+  if (a.slices < 1) return hipErrorInvalidValue;
   const dim3 grid(4 * a.slices, a.nctus, nframes);
   const size_t lds = search_lds_bytes(alt_refs);
   if (alt_refs)

@@ -97,8 +97,9 @@ std::vector<uint8_t> build_tables() {
 // Per-quadrant work lists.  The CUs of one size class inside quadrant q (several shapes
 // share a class) are split into groups of at most class_slots() CUs; a group and a range
 // of its mode pairs form a wave task.  Tasks are cut so that none exceeds half of a wave's
-// fair share, then assigned to the `bins` task lists of the quadrant longest-first onto
-// the least-loaded list.  Costs are VALU-instruction estimates per lane.
+// fair share, then assigned longest-first to the least-loaded of the quadrant's `slices`
+// lists (one per workgroup); each list stays in decreasing cost order, and the waves of a
+// workgroup take its tasks dynamically.  Costs are VALU-instruction estimates per lane.
 // MIPGPU_SHAPE_FILTER="i,j,..." (profiling knob) restricts the search to those shapes.
 struct WorkLists {
   std::vector<mipgpu::WaveTask> tasks;
@@ -135,7 +136,7 @@ double pair_cost(int cls, int ncu) {
   return blocks * 200.0 + mfma * 12.0 + 40.0;
 }
 
-WorkLists build_work(int bins) {
+WorkLists build_work(int slices, int waves) {
   WorkLists wl;
   for (int q = 0; q < 4; q++) {
     struct Piece { mipgpu::WaveTask t; double cost; };
@@ -171,7 +172,7 @@ WorkLists build_work(int bins) {
       }
     }
     // cut long tasks into pair ranges
-    const double cap = total / bins / cut_factor();
+    const double cap = total / (slices * waves) / cut_factor();
     std::vector<Piece> cut;
     for (const Piece &p : pieces) {
       const int np = p.t.q1 - p.t.q0;
@@ -185,6 +186,7 @@ WorkLists build_work(int bins) {
       }
     }
     std::stable_sort(cut.begin(), cut.end(), [](const Piece &a, const Piece &b) { return a.cost > b.cost; });
+    const int bins = slices;
     std::vector<double> load(bins, 0.0);
     std::vector<std::vector<mipgpu::WaveTask>> lists(bins);
     for (const Piece &p : cut) {
@@ -221,7 +223,7 @@ struct mip_engine {
   mipgpu::Job *d_jobs = nullptr;
   int *d_lists = nullptr;
   uint8_t *d_tables = nullptr;
-  int slices = 1, bins = 8;
+  int slices = 1;
 };
 
 extern "C" {
@@ -324,8 +326,7 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   ALLOC(e->d_best, ncu);
   ALLOC(e->d_best_cost, ncu * 4);
   e->slices = o.slices_per_ctu > 0 ? o.slices_per_ctu : 1;
-  e->bins = e->slices * mipgpu::search_waves_per_group();
-  const WorkLists wl = build_work(e->bins);
+  const WorkLists wl = build_work(e->slices, mipgpu::search_waves_per_group());
   ALLOC(e->d_tasks, std::max<size_t>(1, wl.tasks.size()) * sizeof(mipgpu::WaveTask));
   ALLOC(e->d_jobs, std::max<size_t>(1, wl.jobs.size()) * sizeof(mipgpu::Job));
   ALLOC(e->d_lists, wl.list_begin.size() * sizeof(int));
@@ -380,8 +381,41 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.ctu_cols = e->ctu_cols;
   a.nctus = e->nctus;
   a.slices = e->slices;
-  a.bins = e->bins;
+  // MIPGPU_WAVE_TIMING=file (profiling): per-task cycles appended to `file` (synchronous;
+  // one binary record of uint64 [workgroup][wave][kClockSlots] per launch), and the task
+  // lists to `file`.tasks once.
+  static const char *timing = getenv("MIPGPU_WAVE_TIMING");
+  std::vector<uint64_t> clocks;
+  if (timing) {
+    const size_t n = (size_t)4 * e->slices * e->nctus * nframes * mipgpu::kClockSlots;
+    HIP_TRY(hipMalloc((void **)&a.wave_clock, n * 8));
+    HIP_TRY(hipMemsetAsync(a.wave_clock, 0, n * 8, s));
+    clocks.resize(n);
+    static bool dumped = false;
+    if (!dumped) {
+      dumped = true;
+      const WorkLists wl = build_work(e->slices, mipgpu::search_waves_per_group());
+      if (FILE *f = fopen((std::string(timing) + ".tasks").c_str(), "w")) {
+        fprintf(f, "{\"slices\": %d, \"list_begin\": [", e->slices);
+        for (size_t i = 0; i < wl.list_begin.size(); i++) fprintf(f, "%s%d", i ? ", " : "", wl.list_begin[i]);
+        fprintf(f, "], \"tasks\": [");
+        for (size_t i = 0; i < wl.tasks.size(); i++)
+          fprintf(f, "%s[%d, %d, %d, %d]", i ? ", " : "", wl.tasks[i].cls, wl.tasks[i].ncu, wl.tasks[i].q0, wl.tasks[i].q1);
+        fprintf(f, "]}\n");
+        fclose(f);
+      }
+    }
+  }
   HIP_TRY(mipgpu::launch_search(a, nframes, alt, s));
+  if (timing) {
+    HIP_TRY(hipMemcpyAsync(clocks.data(), a.wave_clock, clocks.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    (void)hipFree(a.wave_clock);
+    if (FILE *f = fopen(timing, "ab")) {
+      fwrite(clocks.data(), 8, clocks.size(), f);
+      fclose(f);
+    }
+  }
   if (d_best || d_best_cost) {
     mipgpu::BestArgs b{d_costs, d_best, d_best_cost, nframes * e->nctus * MIP_CUS_PER_CTU};
     HIP_TRY(mipgpu::launch_best_modes(b, s));
