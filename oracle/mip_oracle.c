@@ -290,6 +290,24 @@ void mipo_best_modes(const int32_t *cost, int nctus, uint8_t *best_mode, int32_t
 
 /* --------------------------------------------------------------------- filters --- */
 
+#include "rcp_table.h"
+
+/* The reference's float division v / s as compiled by the AMD OpenCL compiler for gfx950
+ * (disassembly of oracle/_ref): v = mv * 2^ev, s = ms * 2^es (frexp), q = mv * rcp(ms)
+ * with the hardware v_rcp_f32 (1 ulp; e.g. rcp(0.75) = 0x3faaaaaa), result ldexp(q, ev-es).
+ * rcp values: rcp_table.h, captured on an MI355X by tools/rcp_table.hip.  The scales of
+ * the filters are integers 1..1024. */
+static float ref_fdiv(float v, int s) {
+  int es, ev;
+  (void)frexpf((float)s, &es);
+  float rcp;
+  const unsigned bits = MIPO_RCP_TABLE[s - 1];
+  memcpy(&rcp, &bits, 4);
+  const float mv = frexpf(v, &ev);
+  const volatile float q = mv * rcp; /* one fp32 rounding, as v_mul_f32 */
+  return ldexpf(q, ev - es);
+}
+
 /* Validity of a tap at tile-relative (ty, tc) for the 2-D quarter-CTU kernels.  The
  * tile is 128x32 at (qx, qy); gates restate the halo fetch conditions:
  *   3x3: intra.cl:2903-2966, 5x5: intra.cl:3096-3189 (and the float twins).
@@ -328,15 +346,210 @@ static void filter_2d(const uint16_t *in, uint16_t *out, int W, int H, const uin
           scale += c;
         }
       int v;
-      if (is_float) v = (int)roundf((float)sum / (float)scale); /* intra.cl:1794, 2507 */
+      if (is_float) v = (int)roundf(ref_fdiv((float)sum, scale)); /* intra.cl:1794, 2507 */
       else v = (sum + scale / 2) / scale;                         /* intra.cl:3011, 3235 */
       out[(size_t)y * W + x] = (uint16_t)v;
+    }
+}
+
+/* ------------------------------------------------------- separable (1-D) filters ---
+ * filterFrame_1d_{int,float} (intra.cl:3267, 1828) and filterFrame_1d_{int,float}_5x5
+ * (intra.cl:3508, 2539), restated per 128x32 quarter-CTU tile:
+ *  - taps t = row 0 of the 2-D kernel, applied horizontally and then vertically;
+ *  - the tile (+1 / +2 sample halo) is gathered with the reference's own fetch conditions
+ *    (including the ones stricter than "inside the frame": right halo columns need
+ *    x < W-1, bottom halo rows / corners need y < H-1 resp. H-2, see below); samples
+ *    that are not fetched count as 0 (3-tap) or are dropped (5-tap: marker -1 -> 0);
+ *    interior samples below the frame (3-tap tiles read them unguarded, intra.cl:3330)
+ *    are taken as 0, which is what the reference reads from zeroed padding; so are
+ *    interior samples right of the frame (W % 128 != 0, where the reference's linear
+ *    index would wrap -- documented deviation), while halo rows keep the reference's
+ *    linear-index reads;
+ *  - 3-tap scale: (2+t1)^2 inside, (1+t1)(2+t1) on a frame edge row/column, (1+t1)^2 in
+ *    a corner (t0 = t2 = 1 for every kernel of the library) (intra.cl:3281-3285);
+ *  - 5-tap: horizontal sums only for tile rows inside the frame; vertical: each invalid
+ *    row drops its tap weight from the 2-D full scale, then position classes (outer /
+ *    inner edge rows and columns, corners, "interface") select 2-D sub-sums of the 5x5
+ *    kernel as the scale (intra.cl:3523-3557, 3745-3790);
+ *  - rounding: int (v + s/2)/s, float round(v/s) on float operands. */
+static void filter_1d_tile3(const uint16_t *in, uint16_t *out, int W, int H, int X, int Y,
+                            const uint16_t *taps, int is_float) {
+  enum { P = 130, R = 34 };
+  static int16_t tile[R * P];
+  static double hp[R * P];
+  const int t0 = taps[0], t1 = taps[1], t2 = taps[2];
+  memset(tile, 0, sizeof tile);
+  for (int r = 0; r < 32; r++)
+    for (int c = 0; c < 128; c++) {  /* unguarded interior fetch: outside the frame -> 0 */
+      const int y = Y + r, x = X + c;
+      tile[(r + 1) * P + c + 1] = (y < H && x < W) ? (int16_t)in[(size_t)y * W + x] : 0;
+    }
+  const long long WH = (long long)W * H;
+  for (int side = 0; side < 2; side++)  /* top (row Y-1) and bottom (row Y+32) halo rows */
+    for (int c = 0; c < 128; c++) {
+      const long long idx = (long long)(Y - 1 + 33 * side) * W + X + c;
+      if (idx > 0 && idx < WH) tile[(33 * side) * P + 1 + c] = (int16_t)in[idx];
+    }
+  for (int r = 1; r <= 32; r++)       /* left (X-1) and right (X+128) halo columns */
+    for (int side = 0; side < 2; side++) {
+      const long long idx = (long long)(Y + r - 1) * W + X - 1 + 129 * side;
+      if (idx > 0 && idx < WH && X + side > 0 && X + 129 * side < W - 1) tile[r * P + 129 * side] = (int16_t)in[idx];
+    }
+  const long long b = (long long)Y * W + X;
+  if (b - W - 1 > 0 && X > 0 && Y > 0) tile[0] = (int16_t)in[b - W - 1];
+  if (b - W + 128 > 0 && X + 128 < W - 1 && Y > 0) tile[129] = (int16_t)in[b - W + 128];
+  if (b + 32LL * W - 1 < WH && X > 0 && Y + 32 < H - 1) tile[33 * P] = (int16_t)in[b + 32LL * W - 1];
+  if (b + 32LL * W + 128 < WH && X + 128 < W - 1 && Y + 32 < H - 1) tile[33 * P + 129] = (int16_t)in[b + 32LL * W + 128];
+  for (int r = 0; r < R; r++)         /* horizontal pass (halo rows included) */
+    for (int c = 1; c <= 128; c++)
+      hp[r * P + c] = (double)tile[r * P + c - 1] * t0 + (double)tile[r * P + c] * t1 + (double)tile[r * P + c + 1] * t2;
+  const int full = 4 * t0 + 4 * t1 + t1 * t1, corner = t0 + 2 * t1 + t1 * t1, edge = 2 * t0 + 3 * t1 + t1 * t1;
+  const int rows = H - Y < 32 ? H - Y : 32;
+  for (int r = 0; r < rows; r++)
+    for (int c = 0; c < 128 && X + c < W; c++) {
+      const int y = Y + r, x = X + c;
+      const int nb = (y == 0) + (y == H - 1) + (x == 0) + (x == W - 1);
+      const int sc = nb >= 2 ? corner : (nb ? edge : full);
+      const int k = (r + 1) * P + c + 1;
+      const double v = hp[k - P] * t0 + hp[k] * t1 + hp[k + P] * t2;
+      int res;
+      if (is_float) res = (int)roundf(ref_fdiv((float)v, sc));
+      else res = ((int)v + sc / 2) / sc;
+      out[(size_t)y * W + x] = (uint16_t)res;
+    }
+}
+
+static void filter_1d_tile5(const uint16_t *in, uint16_t *out, int W, int H, int X, int Y,
+                            const uint16_t *k2d, int is_float) {
+  enum { P = 132, R = 36 };
+  static int16_t tile[R * P];
+  static double hp[R * P];
+  static int hv[R];
+  const uint16_t *t = k2d; /* row 0 */
+  int full = 0, oc = 0, ic = 0, itf = 0, oe = 0, ie = 0;
+  for (int i = 0; i < 5; i++)
+    for (int j = 0; j < 5; j++) {
+      const int v = k2d[i * 5 + j];
+      full += v;
+      if (i >= 2 && j >= 2) oc += v;
+      if (i >= 1 && j >= 1) ic += v;
+      if (i >= 1 && j >= 2) itf += v;
+      if (j >= 2) oe += v;
+      if (j >= 1) ie += v;
+    }
+  for (int i = 0; i < R * P; i++) tile[i] = -1;
+  const long long WH = (long long)W * H, b = (long long)Y * W + X;
+  for (int r = 0; r < 32; r++)
+    if (Y + r < H)
+      for (int c = 0; c < 128; c++) tile[(r + 2) * P + c + 2] = X + c < W ? (int16_t)in[(size_t)(Y + r) * W + X + c] : 0;
+  for (int r = 0; r < 2; r++)         /* top halo rows Y-2, Y-1 */
+    for (int c = 0; c < 128; c++) {
+      const long long idx = b - 2LL * W + (long long)r * W + c;
+      if (idx > 0 && idx < WH && Y > 0) tile[r * P + 2 + c] = (int16_t)in[idx];
+    }
+  for (int r = 34; r < 36; r++)       /* bottom halo rows Y+32, Y+33: need Y + r < H - 1 */
+    for (int c = 0; c < 128; c++) {
+      const long long idx = b - 2LL * W + (long long)r * W + c;
+      if (idx > 0 && idx < WH && Y + r < H - 1) tile[r * P + 2 + c] = (int16_t)in[idx];
+    }
+  for (int r = 0; r < 32; r++)        /* side halo columns X-2, X-1, X+128, X+129 */
+    for (int q = 0; q < 4; q++) {
+      const int c = q < 2 ? q : q + 128;
+      const long long idx = b - 2 + (long long)r * W + c;
+      if (idx > 0 && idx < WH && X - 2 + c > 0 && X - 2 + c < W - 1) tile[(2 + r) * P + c] = (int16_t)in[idx];
+    }
+  if (X > 0 && Y > 0) {
+    tile[0] = (int16_t)in[b - 2 * W - 2];
+    tile[1] = (int16_t)in[b - 2 * W - 1];
+    tile[P] = (int16_t)in[b - W - 2];
+    tile[P + 1] = (int16_t)in[b - W - 1];
+  }
+  if (Y > 0) {
+    if (X + 128 < W - 1) {
+      tile[P - 2] = (int16_t)in[b - 2 * W + 128];
+      tile[2 * P - 2] = (int16_t)in[b - W + 128];
+    }
+    if (X + 129 < W - 1) {
+      tile[P - 1] = (int16_t)in[b - 2 * W + 129];
+      tile[2 * P - 1] = (int16_t)in[b - W + 129];
+    }
+  }
+  if (X > 0) {
+    if (Y + 32 < H - 1) {
+      tile[34 * P] = (int16_t)in[b + 32LL * W - 2];
+      tile[34 * P + 1] = (int16_t)in[b + 32LL * W - 1];
+    }
+    if (Y + 33 < H - 1) {
+      tile[35 * P] = (int16_t)in[b + 33LL * W - 2];
+      tile[35 * P + 1] = (int16_t)in[b + 33LL * W - 1];
+    }
+  }
+  if (Y + 32 < H - 1 && X + 129 < W - 1) tile[35 * P - 1] = (int16_t)in[b + 32LL * W + 129];
+  if (Y + 32 < H - 1 && X + 128 < W - 1) tile[35 * P - 2] = (int16_t)in[b + 32LL * W + 128];
+  if (Y + 33 < H - 1 && X + 129 < W - 1) tile[36 * P - 1] = (int16_t)in[b + 33LL * W + 129];
+  if (Y + 33 < H - 1 && X + 128 < W - 1) tile[36 * P - 2] = (int16_t)in[b + 33LL * W + 128];
+  for (int r = 0; r < R; r++) {       /* horizontal pass: tile rows that are frame rows */
+    hv[r] = Y + r - 2 >= 0 && Y + r - 2 < H;
+    if (!hv[r]) continue;
+    for (int c = 2; c < 130; c++) {
+      double acc = 0;
+      for (int d = -2; d <= 2; d++) {
+        const int v = tile[r * P + c + d];
+        acc += (double)(v < 0 ? 0 : v) * t[2 + d];
+      }
+      hp[r * P + c] = acc;
+    }
+  }
+  const int rows = H - Y < 32 ? H - Y : 32;
+  for (int r = 0; r < rows; r++)
+    for (int c = 0; c < 128 && X + c < W; c++) {
+      const int y = Y + r, x = X + c;
+      int sc = full;
+      double v = 0;
+      for (int d = -2; d <= 2; d++) {
+        const int rr = r + 2 + d;
+        if (!hv[rr]) sc -= t[2 + d];
+        else v += hp[rr * P + c + 2] * t[2 + d];
+      }
+      const int otb = y == 0 || y == H - 1, itb = y == 1 || y == H - 2;
+      const int olr = x == 0 || x == W - 1, ilr = x == 1 || x == W - 2;
+      const int o_corner = otb && olr, i_corner = itb && ilr;
+      const int iface = (olr && itb) || (ilr && otb);
+      const int o_edge = !o_corner && !iface && (otb || olr);
+      const int i_edge = !i_corner && !iface && (itb || ilr);
+      if (o_corner) sc = oc;
+      if (i_corner) sc = ic;
+      if (o_edge) sc = oe;
+      if (i_edge) sc = ie;
+      if (iface) sc = itf;
+      int res;
+      if (is_float) res = (int)roundf(ref_fdiv((float)v, sc));
+      else res = ((int)v + sc / 2) / sc;
+      out[(size_t)y * W + x] = (uint16_t)res;
+    }
+}
+
+static void filter_1d(const uint16_t *in, uint16_t *out, int W, int H, int kernel_idx, int five, int is_float) {
+  for (int Y = 0; Y < H; Y += 32)
+    for (int X = 0; X < W; X += 128) {
+      if (five) filter_1d_tile5(in, out, W, H, X, Y, TAPS5 + 25 * kernel_idx, is_float);
+      else filter_1d_tile3(in, out, W, H, X, Y, TAPS3 + 9 * kernel_idx, is_float);
     }
 }
 
 int mipo_filter_frame(const uint16_t *in, uint16_t *out, int width, int height, int filter,
                       int kernel_idx) {
   switch (filter) {
+    case MIPO_FILTER_1D_INT:
+    case MIPO_FILTER_1D_FLOAT:
+      if (kernel_idx < 0 || kernel_idx >= 5) return -1;
+      filter_1d(in, out, width, height, kernel_idx, 0, filter == MIPO_FILTER_1D_FLOAT);
+      return 0;
+    case MIPO_FILTER_1D_INT_5x5:
+    case MIPO_FILTER_1D_FLOAT_5x5:
+      if (kernel_idx < 0 || kernel_idx >= 3) return -1;
+      filter_1d(in, out, width, height, kernel_idx, 1, filter == MIPO_FILTER_1D_FLOAT_5x5);
+      return 0;
     case MIPO_FILTER_2D_INT:
     case MIPO_FILTER_2D_FLOAT:
       if (kernel_idx < 0 || kernel_idx >= 5) return -1;
@@ -349,7 +562,7 @@ int mipo_filter_frame(const uint16_t *in, uint16_t *out, int width, int height, 
                 filter == MIPO_FILTER_2D_FLOAT_5x5);
       return 0;
     default:
-      return -2; /* separable variants: see mipo_filter_frame_1d (not yet restated) */
+      return -1;
   }
 }
 

@@ -166,6 +166,14 @@ int main(int argc, char **argv) {
   const size_t pad = (size_t)W * 256 + 4096;
   cl_mem m_ref = clCreateBuffer(ctx, CL_MEM_READ_WRITE, (slots * fs + pad) * 2, NULL, &err); CHECK(err, "buf");
   cl_mem m_filt = clCreateBuffer(ctx, CL_MEM_READ_WRITE, (slots * fs + pad) * 2, NULL, &err); CHECK(err, "buf");
+  /* Zero both frame buffers: the separable filters read rows below the frame unguarded
+   * (intra.cl:3330-3332); with zeros there they compute the in-frame filter. */
+  {
+    const cl_short zero = 0;
+    CHECK(clEnqueueFillBuffer(q, m_ref, &zero, sizeof zero, 0, (slots * fs + pad) * 2, 0, NULL, NULL), "fill");
+    CHECK(clEnqueueFillBuffer(q, m_filt, &zero, sizeof zero, 0, (slots * fs + pad) * 2, 0, NULL, NULL), "fill");
+    CHECK(clFinish(q), "fill finish");
+  }
   cl_mem m_redT = clCreateBuffer(ctx, CL_MEM_READ_WRITE, slots * nctus * RED_PER_CTU * 2, NULL, &err); CHECK(err, "buf");
   cl_mem m_redL = clCreateBuffer(ctx, CL_MEM_READ_WRITE, slots * nctus * RED_PER_CTU * 2, NULL, &err); CHECK(err, "buf");
   cl_mem m_refT = clCreateBuffer(ctx, CL_MEM_READ_WRITE, slots * nctus * REF_PER_CTU * 2, NULL, &err); CHECK(err, "buf");

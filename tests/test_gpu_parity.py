@@ -1,8 +1,8 @@
 """HIP path parity: libmipgpu.so (gfx950 kernels) against the C oracle and against the
 reference kernels' golden outputs.  Integer path -> bit-exact everywhere; the float
-filters are also required to be bit-exact (tolerance 0: correctly rounded fp32 division
-makes round(sum/scale) equal the integer rounding, and the reference agreed on every
-fixture)."""
+filters are also required to be bit-exact (tolerance 0): both sides divide exactly as
+the reference's compiled kernels do (frexp / v_rcp_f32 / v_mul / v_ldexp, see
+oracle/mip_oracle.c ref_fdiv), which the golden fixtures with tie-prone scales pin."""
 import numpy as np
 import pytest
 
@@ -13,8 +13,9 @@ from mipgpu.synth import synth_frame, synth_frames
 
 pytestmark = pytest.mark.gpu
 
-FILTERS_2D = [("filterFrame_2d_int_quarterCtu", 5), ("filterFrame_2d_float_quarterCtu", 5),
-              ("filterFrame_2d_int_5x5_quarterCtu", 3), ("filterFrame_2d_float_5x5_quarterCtu", 3)]
+FILTERS = [("filterFrame_1d_int", 5), ("filterFrame_1d_float", 5), ("filterFrame_2d_int_quarterCtu", 5),
+           ("filterFrame_2d_float_quarterCtu", 5), ("filterFrame_1d_int_5x5", 3), ("filterFrame_1d_float_5x5", 3),
+           ("filterFrame_2d_int_5x5_quarterCtu", 3), ("filterFrame_2d_float_5x5_quarterCtu", 3)]
 
 
 def _engine(c, **kw):
@@ -61,7 +62,7 @@ def test_full_size_configs_vs_reference(gpu_available, name):
             assert G.sha(filt[f]) == fr["filtered_sha256"]
 
 
-@pytest.mark.parametrize("filt,nk", FILTERS_2D)
+@pytest.mark.parametrize("filt,nk", FILTERS)
 def test_filters_vs_oracle(gpu_available, filt, nk):
     frame = synth_frame(392, 136, 0x51, 1)  # partial tiles on both axes
     with MipEngine(392, 136) as eng:

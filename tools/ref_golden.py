@@ -44,6 +44,19 @@ CONFIGS = {
     "c3_1080p_alt_float5": (1920, 1080, 2, 0, 0x1081, "filterFrame_2d_float_5x5_quarterCtu", 2, False, [0, 70]),
     "c1_1080p_uniform": (1920, 1080, 1, 1, 0x1082, None, 0, False, [5]),
     "c5_2160p_alt_int": (3840, 2160, 1, 0, 0x2160, "filterFrame_2d_int_quarterCtu", 0, False, [0, 509]),
+    # separable filters (frame buffers zeroed by ref_runner; <= 2 frames so that rows read
+    # below a frame are zeros, see oracle/mip_oracle.c filter_1d_tile3)
+    "small_sep_1d_int": (384, 256, 2, 0, 0x3B0, "filterFrame_1d_int", 1, True, [0, 4]),
+    "small_sep_1d_float": (256, 200, 2, 0, 0x3B1, "filterFrame_1d_float", 4, False, [0, 2]),
+    "small_sep_1d_int_k3": (256, 256, 1, 1, 0x3B4, "filterFrame_1d_int", 3, False, [1]),
+    "small_sep_1d_int5": (384, 232, 1, 1, 0x3B2, "filterFrame_1d_int_5x5", 2, False, [1]),
+    "small_sep_1d_float5": (256, 136, 2, 0, 0x3B3, "filterFrame_1d_float_5x5", 1, False, [2]),
+    "small_sep_1d_int5_k0": (128, 104, 1, 0, 0x3B5, "filterFrame_1d_int_5x5", 0, False, [0]),
+    "c3s_1080p_sep_float5": (1920, 1080, 1, 0, 0x1083, "filterFrame_1d_float_5x5", 2, False, [0, 70]),
+    "c3s_1080p_sep_int": (1920, 1080, 1, 0, 0x1084, "filterFrame_1d_int", 2, False, [16]),
+    # float filters with scales whose fp32 quotient ties depend on the reference's division
+    "small_alt_2d_float3_k2": (384, 256, 1, 0, 0x3A6, "filterFrame_2d_float_quarterCtu", 2, False, [0, 4]),
+    "small_alt_2d_float3_k4": (256, 264, 1, 1, 0x3A7, "filterFrame_2d_float_quarterCtu", 4, False, [1]),
 }
 
 

@@ -203,7 +203,7 @@ WorkLists build_work(int slices, int waves) {
   return wl;
 }
 
-bool filter_supported(int f) { return f == 2 || f == 3 || f == 6 || f == 7; }
+bool filter_supported(int f) { return f >= 0 && f <= 7; }
 bool filter_valid(int f, int k) {
   if (f < 0 || f > 7) return false;
   const bool five = f >= 4;
