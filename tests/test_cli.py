@@ -1,0 +1,121 @@
+"""CLI surface: vvc-mip-gpu_amd/bin/mipgpu_cli against the reference's main.cpp contract.
+
+* argument handling and exit codes of main.cpp:47-83 / main_aux_functions.h:113-162
+  (CPU: these paths end before an engine is created);
+* the cost log, byte for byte, against a restatement of exportAllDistortionValues_File
+  (main_aux_functions.h:735-798) filled with the C oracle's costs (GPU)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from mipgpu import layout
+from mipgpu.synth import synth_frames
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(REPO, "vvc-mip-gpu_amd", "bin", "mipgpu_cli")
+
+needs_cli = pytest.mark.skipif(not os.path.exists(CLI), reason="CLI not built (make -C vvc-mip-gpu_amd)")
+
+
+def run(args, timeout=300):
+    return subprocess.run([CLI] + args, capture_output=True, text=True, timeout=timeout)
+
+
+def reference_log(cost, width, sad=None, satd=None) -> bytes:
+    """exportAllDistortionValues_File (main_aux_functions.h:735-798) for one frame: header,
+    then per CTU the SizeId2, SizeId1 and SizeId0 shapes in table order, every CU, every
+    mode (transposed ones included); X/Y from ALL_X_POS/ALL_Y_POS, 4x4 CUs from
+    4*(cu%32), 4*(cu/32) (785-786); SAD, SATD, minSadHad printed with %ld."""
+    nctus = cost.size // layout.COSTS_PER_CTU
+    ctu_cols = -(-width // 128)
+    out = ["CTU,cuSizeName,W,H,CU,X,Y,Mode,SAD,SATD,minSadHad\n"]
+    for ctu in range(nctus):
+        cx, cy = 128 * (ctu % ctu_cols), 128 * (ctu // ctu_cols)
+        for s in layout.SHAPES:
+            if s.size_id == 0:
+                xs = 4 * (np.arange(s.ncu) % 32)
+                ys = 4 * (np.arange(s.ncu) // 32)
+            else:
+                xs, ys = s.positions()
+            for cu in range(s.ncu):
+                head = f"{ctu},{s.name},{s.w},{s.h},{cu},{cx + xs[cu]},{cy + ys[cu]},"
+                base = ctu * layout.COSTS_PER_CTU + s.cost_offset + cu * s.total_modes
+                for m in range(s.total_modes):
+                    i = base + m
+                    a = 0 if sad is None else sad[i]
+                    b = 0 if satd is None else satd[i]
+                    out.append(f"{head}{m},{a},{b},{cost[i]}\n")
+    return "".join(out).encode()
+
+
+def write_csv(path, frames):
+    with open(path, "w") as f:
+        for fr in frames:
+            for row in fr:
+                f.write(",".join(map(str, row.tolist())) + "\n")
+
+
+def mask_unavailable(cost, width, height):
+    m = layout.available_mask(width, height)
+    return np.where(m, cost, layout.UNAVAILABLE).astype(np.int32)
+
+
+# ---------------------------------------------------------------- CPU: arguments
+@needs_cli
+def test_help_exits_1():
+    r = run(["-h"])
+    assert r.returncode == 1 and "--FramesToBeEncoded" in r.stdout
+
+
+@needs_cli
+def test_missing_parameters_are_reported():
+    r = run(["-s", "64x64"])
+    assert r.returncode == 1
+    assert "[!] ERROR: FramesToBeEncoded not set." in r.stdout
+    assert "[!] ERROR: Input original frames not set." in r.stdout
+    assert "Exiting after finding errors in input parameters" in r.stdout
+
+
+@needs_cli
+def test_unsupported_filter_exits_0():
+    r = run(["-f", "1", "-s", "64x64", "-o", "x.csv", "--FilterType=notAFilter"])
+    assert r.returncode == 0 and "Filter type notAFilter not supported" in r.stdout
+
+
+@needs_cli
+def test_unknown_and_ambiguous_options():
+    assert run(["--Bogus", "1"]).returncode == 1
+    assert "ambiguous" in run(["--F", "1"]).stderr  # FramesToBeEncoded / FilterType
+
+
+# ------------------------------------------------------------ GPU: the cost log
+@pytest.mark.gpu
+@needs_cli
+@pytest.mark.parametrize("extra,filt,kidx,sad_satd", [
+    ([], None, 0, False),
+    (["--FilterType", "filterFrame_2d_int_quarterCtu", "--KernelIdx", "1"], "filterFrame_2d_int_quarterCtu", 1, False),
+    (["--Filter=filterFrame_1d_float_5x5", "--KernelIdx=2", "--ReportSadSatd"], "filterFrame_1d_float_5x5", 2, True),
+])
+def test_cost_log_is_byte_identical(gpu_available, tmp_path, extra, filt, kidx, sad_satd):
+    W, H, N = 256, 136, 2
+    frames = synth_frames(W, H, N, 0xC11, 1)
+    write_csv(tmp_path / "in.csv", frames)
+    prefix = str(tmp_path / "out")
+    r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / "in.csv"), "-l", prefix] + extra)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for f in range(N):
+        assert f"Current frame {f}\n" in r.stdout
+    assert re.search(rf"Elapsed time \(ms\) from writing samples to reading distortion \({N}x\), \d+\n", r.stdout)
+    refs = None if filt is None else O.filter_frame(frames[0], filt, kidx)
+    res = O.search(frames[0], refs, want_sad_satd=sad_satd)
+    cost, sad, satd = res if sad_satd else (res, None, None)
+    cost = mask_unavailable(cost, W, H)
+    if sad_satd:
+        sad, satd = mask_unavailable(sad, W, H), mask_unavailable(satd, W, H)
+    got = open(prefix + ".csv", "rb").read()
+    want = reference_log(cost, W, sad, satd)
+    assert len(got) == len(want) and got == want

@@ -7,7 +7,7 @@ path is the HIP library only: if it is missing this module raises at import of
 Mirrors the reference's operator surface (main.cpp + main_aux_functions.h):
   * filter names / KernelIdx of the reference whitelist (constants.h:25-34),
   * the per-frame cost table in the reference layout (constants.h:1558-1631),
-  * the CSV cost log (``mipgpu.log.write_cost_log``, main_aux_functions.h:735-798).
+  * the CSV cost log is written by the C++ CLI (``bin/mipgpu_cli``, main_aux_functions.h:735-798).
 """
 from __future__ import annotations
 
