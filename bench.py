@@ -14,9 +14,15 @@ Rank 0 prints one JSON line (contract in the task statement), plus:
   roofline      HBM roofline of the search kernel (algorithmic bytes = frame read + int32
                 cost write, per launch) with the launch time from HIP events on the stream
                 the kernel runs on, and the PMC-measured traffic when profiles/ holds it;
-  valu          the same launch priced in algorithmic integer ops (SURVEY.md section 8d
-                model, 140.3 M ops per CTU) against the VALU int32 rate -- the bound that
-                actually applies to this path;
+  valu          the bound that actually applies to this path: VALU instruction issue.
+                Wave64 VALU instructions per launch (PMC SQ_INSTS_VALU, profiles/traffic.json)
+                over the live launch time against the chip's issue rate (1024 SIMDs x one
+                wave64 instruction per 4 cycles at 2.4 GHz), plus the measured issue
+                utilization; the SURVEY 8d algorithmic op count is reported alongside;
+  filter        the alternative-reference low-pass filter of BASELINE configs[2]
+                (filterFrame_2d_float_5x5_quarterCtu, KernelIdx 2) on the same frames:
+                HBM roofline (one frame read + one write per frame) and the alt-refs
+                search rate (filter + search per step);
   cpu_baseline  the C oracle (oracle/mip_oracle.c, OpenMP) on the host cores, one full frame;
   reference_gpu the reference's own OpenCL kernels (oracle/_ref, compiled from intra.cl)
                 timed on the same MI355X, when their code objects are present;
@@ -35,9 +41,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "1080p frames/sec, full MIP mode search over all CU sizes; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E peak (spec)
-# VALU: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz = 39.3 T lane-ops/s (a wave64 VALU op issues
-# in 4 cycles, MI355X_MICROARCH.md); the kernel computes in packed int16 (2 ops per lane-op).
-VALU_PEAK_OPS = 256 * 4 * 16 * 2 * 2.4e9
+# VALU issue: 256 CUs x 4 SIMDs, one wave64 instruction per 4 cycles each, 2.4 GHz
+# (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s.
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
 # SURVEY.md section 8d algorithmic op model per CTU: GEMV 40.4 M MAC (on MFMA here) and
 # 99.6 M vector ops (upsampling 13.8 + 19.9 M, SAD 19.3 M, SATD 46.6 M) -- the VALU share.
 VECTOR_OPS_PER_CTU = 99.6e6
@@ -80,6 +86,56 @@ def load_pmc(width, height, frames):
         return json.load(open(path)).get("%dx%dx%d" % (width, height, frames), {})
     except Exception:
         return {}
+
+
+def valu_section(pmc, kernel_ms, alg_ops):
+    insts = pmc.get("valu_insts_per_launch")
+    out = {"bound": "valu-issue", "unit": "G wave64 VALU instructions/s", "peak": round(VALU_PEAK_INSTS / 1e9, 1),
+           "achieved": None, "frac": None, "valu_insts_per_launch": insts,
+           "issue_utilization": pmc.get("valu_issue_utilization"),
+           "algorithmic_vector_ops_per_s": round(alg_ops / (kernel_ms * 1e-3) / 1e12, 2),
+           "algorithmic_unit": "T int ops/s (SURVEY 8d model, 99.6 M vector ops per CTU)"}
+    if insts:
+        rate = insts / (kernel_ms * 1e-3)
+        out["achieved"], out["frac"] = round(rate / 1e9, 1), round(rate / VALU_PEAK_INSTS, 4)
+    return out
+
+
+def filter_section(eng_cls, frames, W, H, B, stream, dev, steps, pmc):
+    """BASELINE configs[2] filter (2-D float 5x5, KernelIdx 2) on the resident frames: HBM
+    roofline of the filter kernel and the alternative-reference search rate."""
+    import torch
+    from mipgpu import filter_device
+    name, kidx = "filterFrame_2d_float_5x5_quarterCtu", 2
+    out = torch.empty_like(frames)
+    for _ in range(3):
+        filter_device(frames, out, name, kidx, stream=stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        filter_device(frames, out, name, kidx, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    alg = 2 * 2 * W * H * B
+    res = {"kernel": "filter2d_kernel<5x5, float>", "filter": name, "kernel_idx": kidx, "bound": "hbm",
+           "kernel_ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": alg,
+           "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "traffic": (pmc.get("filter") or {}).get("hbm_bytes_per_launch")}
+    alt = eng_cls(W, H, device=dev.index, filter=name, kernel_idx=kidx, max_batch=B)
+    costs = torch.empty((B, alt.costs_per_frame), dtype=torch.int32, device=dev)
+    for _ in range(2):
+        alt.search_device(frames, costs=costs, stream=stream)
+    e0.record(stream)
+    for _ in range(steps):
+        alt.search_device(frames, costs=costs, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    res["alt_refs_search"] = {"value": round(B * steps / (e0.elapsed_time(e1) * 1e-3), 1), "unit": "frames/s",
+                              "note": "filter + search per step, device time (BASELINE configs[2] path)"}
+    alt.close()
+    return res
 
 
 def cpu_baseline(width, height, seed, budget_s=10.0):
@@ -134,6 +190,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-reference-gpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency launches")
+    ap.add_argument("--no-filter", action="store_true", help="skip the filter / alternative-refs measurement")
     args = ap.parse_args()
 
     import numpy as np
@@ -197,15 +254,11 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc.get("hbm_bytes_per_launch"),
                          "kernel": "mip_search_kernel", "kernel_ms_per_launch": round(max_kernel_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
-            # The bound that applies: VALU issue.  `frac` prices the algorithmic vector ops
-            # (SURVEY 8d model) at the packed-int16 rate; `issue_utilization` is measured
-            # (PMC SQ_INSTS_VALU x 4 cycles / SIMD cycles, profiles/traffic.json).
-            "valu": {"achieved": round(ops / (max_kernel_ms * 1e-3) / 1e12, 3), "peak": round(VALU_PEAK_OPS / 1e12, 2),
-                     "unit": "Tops/s (algorithmic vector int ops, SURVEY 8d model; peak = packed-int16 VALU rate)",
-                     "frac": round(ops / (max_kernel_ms * 1e-3) / VALU_PEAK_OPS, 4),
-                     "issue_utilization": pmc.get("valu_issue_utilization"),
-                     "valu_insts_per_launch": pmc.get("valu_insts_per_launch")},
+            # The bound that applies: VALU issue (see the module docstring).
+            "valu": valu_section(pmc, max_kernel_ms, ops),
         }
+        if world == 1 and not args.no_filter:
+            res["filter"] = filter_section(MipEngine, frames, W, H, B, stream, dev, 5, pmc)
         if world == 1 and not args.no_latency:
             # Latency of a single-frame launch (informative; `value` is batch throughput).
             f1 = torch.empty((1, eng.costs_per_frame), dtype=torch.int32, device=dev)

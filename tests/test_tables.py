@@ -62,3 +62,22 @@ def test_generated_header_matches_reference():
     assert [s.h for s in layout.SHAPES] == c["ALL_heights"]
     assert [s.ncu for s in layout.SHAPES] == c["ALL_cusPerCtu"]
     assert [s.modes for s in layout.SHAPES] == c["ALL_numPredModes"]
+
+
+def _taps(name):
+    hdr = open(os.path.join(os.path.dirname(TOOLS), "vvc-mip-gpu_amd", "csrc", "mip_tables.h")).read()
+    line = next(l for l in hdr.splitlines() if l.startswith("#define " + name))
+    return [int(v) for v in line[line.index("{") + 1:line.index("}")].split(",")]
+
+
+@pytest.mark.parametrize("name,ks,n", [("MIP_TAPS_3x3", 3, 5), ("MIP_TAPS_5x5", 5, 3)])
+def test_filter_kernels_are_outer_product_plus_centre(name, ks, n):
+    """mip_filter.hip computes every 2-D filter as t (x) t + d * delta with t = row 0 of
+    the kernel (convKernelLib, constants.cl) -- true for every kernel of the library."""
+    taps = np.array(_taps(name)).reshape(n, ks, ks)
+    for k in taps:
+        t = k[0]
+        d = k[ks // 2, ks // 2] - t[ks // 2] ** 2
+        want = np.outer(t, t)
+        want[ks // 2, ks // 2] += d
+        assert np.array_equal(k, want) and (k == k.T).all()

@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Device time and HBM roofline fraction of each of the eight filters (1080p x 32 frames,
+HIP events on the launch stream)."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "vvc-mip-gpu_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mipgpu import FILTERS, filter_device  # noqa: E402
+from mipgpu.synth import synth_frames  # noqa: E402
+
+W, H, B, REPS = 1920, 1080, 32, 20
+frames = torch.from_numpy(synth_frames(W, H, B, 0x1080, 0).astype(np.int16)).cuda()
+out = torch.empty_like(frames)
+s = torch.cuda.Stream()
+res = {}
+for name in FILTERS:
+    for _ in range(3):
+        filter_device(frames, out, name, 0, stream=s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(REPS):
+        filter_device(frames, out, name, 0, stream=s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / REPS
+    gbs = 4 * W * H * B / (ms * 1e-3) / 1e9
+    res[name] = {"ms_per_launch": round(ms, 4), "GB/s": round(gbs, 1), "frac_of_8TB/s": round(gbs / 8000, 3)}
+print(json.dumps({"workload": "%dx%d x %d frames, kernel_idx 0" % (W, H, B), "filters": res}, indent=1))

@@ -12,31 +12,55 @@ import os
 import sys
 
 root, key, out = sys.argv[1], sys.argv[2], sys.argv[3]
-vals = {"FETCH_SIZE": [], "WRITE_SIZE": [], "SQ_INSTS_VALU": [], "GRBM_GUI_ACTIVE": [], "SQ_LDS_BANK_CONFLICT": [],
-        "SQ_LDS_IDX_ACTIVE": []}
-for path in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
-    per = {}
-    for r in csv.DictReader(open(path)):
-        if "mip_search_kernel" not in r["Kernel_Name"] or r["Counter_Name"] not in vals:
-            continue
-        k = (r["Dispatch_Id"], r["Counter_Name"])
-        per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
-    for (_, c), v in per.items():
-        vals[c].append(v)
-fetch = 2 * 1024 * sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
-write = 1024 * sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
-mean = lambda c: sum(vals[c]) / len(vals[c]) if vals[c] else None
-valu, grbm = mean("SQ_INSTS_VALU"), mean("GRBM_GUI_ACTIVE")
+COUNTERS = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE")
+SEARCH = "mip_search_kernel<false>"          # original-reference search (the bench `value`)
+FILTER = "filter2d_kernel<2, true>"          # BASELINE configs[2] filter (bench `filter`)
+
+
+def collect(kernel):
+    vals = {c: [] for c in COUNTERS}
+    for path in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        per = {}
+        for r in csv.DictReader(open(path)):
+            if kernel not in r["Kernel_Name"] or r["Counter_Name"] not in vals:
+                continue
+            k = (r["Dispatch_Id"], r["Counter_Name"])
+            per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
+        for (_, c), v in per.items():
+            vals[c].append(v)
+    return vals
+
+
+def mean(vals, c):
+    return sum(vals[c]) / len(vals[c]) if vals[c] else None
+
+
+def traffic(vals):
+    fetch, write = mean(vals, "FETCH_SIZE"), mean(vals, "WRITE_SIZE")
+    if fetch is None or write is None:
+        return None
+    fetch, write = 2 * 1024 * fetch, 1024 * write
+    return {"hbm_bytes_per_launch": round(fetch + write), "fetch_bytes_x2": round(fetch), "write_bytes": round(write),
+            "dispatches": [len(vals["FETCH_SIZE"]), len(vals["WRITE_SIZE"])]}
+
+
+s_vals = collect(SEARCH)
+rec = traffic(s_vals) or {}
+valu, grbm = mean(s_vals, "SQ_INSTS_VALU"), mean(s_vals, "GRBM_GUI_ACTIVE")
 # GRBM_GUI_ACTIVE is summed over the 8 XCDs; a wave64 VALU instruction issues in 4 cycles on
 # one of the 1024 SIMDs (MI355X_MICROARCH.md).
 util = valu * 4 / (1024 * grbm / 8) if valu and grbm else None
+conf, lds = mean(s_vals, "SQ_LDS_BANK_CONFLICT"), mean(s_vals, "SQ_LDS_IDX_ACTIVE")
+rec.update({"kernel": SEARCH, "valu_insts_per_launch": valu, "gui_active_cycles_per_xcd": grbm and grbm / 8,
+            "valu_issue_utilization": util and round(util, 4),
+            "lds_bank_conflict_frac": conf and lds and round(conf / lds, 4),
+            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/pmc_profile.sh); "
+                      "FETCH_SIZE KiB x1024 x2 (gfx950 correction), WRITE_SIZE KiB x1024"})
+f = traffic(collect(FILTER))
+if f:
+    f["kernel"] = FILTER
+    rec["filter"] = f
 d = json.load(open(out)) if os.path.exists(out) else {}
-d[key] = {"hbm_bytes_per_launch": round(fetch + write), "fetch_bytes_x2": round(fetch), "write_bytes": round(write),
-          "dispatches": [len(vals["FETCH_SIZE"]), len(vals["WRITE_SIZE"])],
-          "valu_insts_per_launch": valu, "gui_active_cycles_per_xcd": grbm and grbm / 8,
-          "valu_issue_utilization": util and round(util, 4),
-          "lds_bank_conflict_frac": mean("SQ_LDS_BANK_CONFLICT") and round(mean("SQ_LDS_BANK_CONFLICT") / mean("SQ_LDS_IDX_ACTIVE"), 4),
-          "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/pmc_profile.sh); "
-                    "FETCH_SIZE KiB x1024 x2 (gfx950 correction), WRITE_SIZE KiB x1024"}
+d[key] = rec
 json.dump(d, open(out, "w"), indent=1)
 print(json.dumps(d[key]))

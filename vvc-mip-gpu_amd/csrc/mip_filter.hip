@@ -1,36 +1,50 @@
 // mip_filter.hip -- LDS-tiled low-pass filters of the reference samples (gfx950).
 //
-// All eight reference filters work per 128x32 quarter-CTU tile plus a 1- or 2-sample
-// halo, because the reference's halo gates are defined per tile; so do these kernels
-// (one workgroup per tile, HBM-bound: one read and one write of the frame).
+// All eight reference filters work per 128x32 quarter-CTU tile plus a 1- or 2-sample halo,
+// because the reference's halo gates are defined per tile; so does this kernel (one
+// 128-thread workgroup per tile; HBM-bound: one read and one write of the frame).
 //  * 2-D (filterFrame_2d_{int,float}[_5x5]_quarterCtu, intra.cl:2856, 1639, 3042, 2311):
-//    a halo cell is loaded when the reference would load it (restated in tap_valid) and
-//    marked invalid (-1) otherwise; each output is the normalised convolution over its
-//    valid taps.
+//    a halo cell is loaded when the reference would load it (tap_valid) and marked invalid
+//    (-1) otherwise; each output is the normalised convolution over its valid taps.
 //  * separable (filterFrame_1d_{int,float}[_5x5], intra.cl:3267, 1828, 3508, 2539): row 0
-//    of the 2-D kernel applied horizontally (halo rows included) and then vertically,
-//    with the reference's fetch conditions (sep_fetch) and its position-class scales
+//    of the 2-D kernel applied horizontally (halo rows included) and then vertically, with
+//    the reference's fetch conditions (sep_fetch) and its position-class scales
 //    (oracle/mip_oracle.c filter_1d_tile3/5 documents the rules).
-// Rounding: int (sum + scale/2) / scale; float round(ref_fdiv(sum, scale)) where
-// ref_fdiv is the reference's own fp32 division sequence (frexp, v_rcp_f32, v_mul,
-// v_ldexp: the AMD OpenCL lowering of '/', read from the reference's code objects),
-// which differs from IEEE division at exact ties for scales like 12 or 24.
+//
+// One computation serves both: every kernel of the library is t (x) t + d * delta, with t =
+// row 0 of the 2-D kernel and d the centre excess (tests/test_tables.py checks this), so
+//    numerator = sum_i t_i * sum_j t_j * max(v_ij, 0)  (+ d * centre for the 2-D filters)
+// is a horizontal pass in packed 16-bit lanes (4 columns per thread, v_pk_mad_u16; sums <=
+// 9 * 1023) followed by a vertical v_dot2 pass.  The 2-D scale is the full kernel sum
+// minus the same separable pass over the invalid-cell indicator (only in tiles that have
+// an invalid cell: frame borders and the reference's stricter halo gates); the separable
+// scale is the reference's closed-form position class.
+// Rounding: int (sum + scale/2) / scale (exact multiply-high for the uniform scale);
+// float round(sum * R(scale)) where R(s) = ldexp(rcp(frexp_mant(s)), -frexp_exp(s)) --
+// exactly the reference's own fp32 division sequence (frexp, v_rcp_f32, v_mul, v_ldexp:
+// the AMD OpenCL lowering of '/', read from the reference's code objects), since scaling
+// by a power of two commutes with the multiply's rounding.
 #include "mip_kernels.h"
 #include "mip_tables.h"
 
 namespace mipgpu {
 namespace {
 
-__device__ __forceinline__ float ref_fdiv(float v, float s) {
-  const float ms = __builtin_amdgcn_frexp_mantf(s);
-  const int es = __builtin_amdgcn_frexp_expf(s);
-  const float mv = __builtin_amdgcn_frexp_mantf(v);
-  const int ev = __builtin_amdgcn_frexp_expf(v);
-  return __builtin_amdgcn_ldexpf(mv * __builtin_amdgcn_rcpf(ms), ev - es);
-}
+typedef short s2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+
+constexpr int kThreads = 128;  // per tile: thread t owns columns 4(t&31).. +3, rows 8(t>>5).. +7
+constexpr int kCO = 10;        // LDS column of tile column 0 (tile column c0-2 is 8-byte aligned)
+constexpr int kTWP = 144;      // LDS row pitch in samples
 
 __constant__ uint16_t c_taps3[5 * 9] = MIP_TAPS_3x3;
 __constant__ uint16_t c_taps5[3 * 25] = MIP_TAPS_5x5;
+
+// The reference's fp32 division v / s as a multiplication (see the header).
+__device__ __forceinline__ float ref_recip(float s) {
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_rcpf(__builtin_amdgcn_frexp_mantf(s)),
+                                 -__builtin_amdgcn_frexp_expf(s));
+}
 
 // Validity of tile cell (ty, tc) of the tile at (qx, qy): 3x3 gates intra.cl:2903-2966,
 // 5x5 gates intra.cl:3096-3189.  Interior cells: inside the frame.
@@ -52,58 +66,13 @@ __device__ __forceinline__ bool tap_valid(int rad, int qx, int qy, int ty, int t
   return g > 0 && g < WH && qx + tc > 0 && qx + tc < W - 1;
 }
 
-template <int RAD, bool FLOAT>
-__global__ __launch_bounds__(256) void filter2d_kernel(FilterArgs a) {
-  constexpr int KS = 2 * RAD + 1;
-  constexpr int TW = 128 + 2 * RAD, TH = 32 + 2 * RAD;
-  constexpr int PITCH = TW + 1;
-  __shared__ short tile[TH * PITCH];
-  const int qx = 128 * blockIdx.x, qy = 32 * blockIdx.y, f = blockIdx.z;
-  const int W = a.width, H = a.height;
-  const uint16_t *in = a.in + (size_t)f * W * H;
-  for (int i = threadIdx.x; i < TH * TW; i += blockDim.x) {
-    const int r = i / TW, c = i - r * TW;
-    const int ty = r - RAD, tc = c - RAD;
-    short v = -1;
-    if (tap_valid(RAD, qx, qy, ty, tc, W, H)) v = (short)in[(size_t)(qy + ty) * W + qx + tc];
-    tile[r * PITCH + c] = v;
-  }
-  __syncthreads();
-  const uint16_t *taps = RAD == 1 ? c_taps3 + 9 * a.kernel_idx : c_taps5 + 25 * a.kernel_idx;
-  int k[KS * KS];
-#pragma unroll
-  for (int i = 0; i < KS * KS; i++) k[i] = taps[i];
-  uint16_t *out = a.out + (size_t)f * W * H;
-  for (int i = threadIdx.x; i < 128 * 32; i += blockDim.x) {
-    const int ty = i >> 7, tc = i & 127;
-    if (qy + ty >= H || qx + tc >= W) continue;
-    int sum = 0, scale = 0;
-#pragma unroll
-    for (int dy = 0; dy < KS; dy++)
-#pragma unroll
-      for (int dx = 0; dx < KS; dx++) {
-        const int v = tile[(ty + dy) * PITCH + tc + dx];
-        const int c = v >= 0 ? k[dy * KS + dx] : 0;
-        sum += c * max(v, 0);
-        scale += c;
-      }
-    int r;
-    if (FLOAT) r = (int)roundf(ref_fdiv((float)sum, (float)scale));
-    else r = (sum + scale / 2) / scale;
-    out[(size_t)(qy + ty) * W + qx + tc] = (uint16_t)r;
-  }
-}
-
-// Separable filters: is tile cell (ty, tc) fetched from the frame (intra.cl:3296-3345
-// for 3 taps, 3566-3640 for 5 taps)?  Cells inside the tile are always fetched by the
-// 3-tap kernels (no bound check; samples below / right of the frame read 0 here) and
-// for rows inside the frame by the 5-tap kernels.
+// Separable filters: is halo cell (ty, tc) fetched from the frame (intra.cl:3296-3345 for
+// 3 taps, 3566-3640 for 5 taps)?
 template <int RAD>
 __device__ __forceinline__ bool sep_fetch(int qx, int qy, int ty, int tc, int W, int H) {
   const long long WH = (long long)W * H;
   const long long g = (long long)(qy + ty) * W + qx + tc;
   const bool top = ty < 0, bot = ty >= 32, lft = tc < 0, rgt = tc >= 128;
-  if (!top && !bot && !lft && !rgt) return RAD == 1 || qy + ty < H;
   if (RAD == 1) {
     if ((top || bot) && (lft || rgt)) {
       const long long b = (long long)qy * W + qx;
@@ -125,88 +94,253 @@ __device__ __forceinline__ bool sep_fetch(int qx, int qy, int ty, int tc, int W,
   return g > 0 && g < WH && qx + tc > 0 && qx + tc < W - 1;
 }
 
-template <int RAD, bool FLOAT>
-__global__ __launch_bounds__(256) void filter1d_kernel(FilterArgs a) {
-  constexpr int KS = 2 * RAD + 1;
-  constexpr int TW = 128 + 2 * RAD, TH = 32 + 2 * RAD;
-  __shared__ short tile[TH * TW];
-  __shared__ int hsum[TH * 128];  // horizontal pass; -1: tile row outside the frame (5 taps)
+// Tile cell inside the 128x32 tile: 2-D -- valid iff inside the frame, else -1; separable
+// 3 taps -- always fetched, samples outside the frame read 0 (intra.cl:3330, unguarded);
+// separable 5 taps -- fetched for frame rows (outside columns read 0), else -1.
+template <int RAD, bool SEP>
+__device__ __forceinline__ short inner_value(const uint16_t *in, int x, int y, int W, int H) {
+  if (y < H && x < W) return (short)in[(size_t)y * W + x];
+  if (!SEP) return -1;
+  return (RAD == 1 || y < H) ? 0 : -1;
+}
+
+// Stage the tile (+halo) in LDS: interior rows with 16-byte loads when the rows are
+// 16-byte aligned (W % 8 == 0), halo cells one by one with the reference's gates.
+// Returns whether this thread stored an invalid (-1) cell.
+template <int RAD, bool SEP>
+__device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, int qy, int W, int H) {
+  constexpr int TW = 128 + 2 * RAD;
+  const int t = threadIdx.x;
+  bool invalid = false;
+  if ((W & 7) == 0) {
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const int i = p * kThreads + t, r = i >> 4, k = i & 15;
+      const int y = qy + r, x = qx + 8 * k;
+      short *dst = tile + (r + RAD) * kTWP + kCO + 8 * k;
+      if (y < H && x + 8 <= W) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(in + (size_t)y * W + x);
+        uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);  // 4-byte aligned (kCO even)
+        d32[0] = v.x;
+        d32[1] = v.y;
+        d32[2] = v.z;
+        d32[3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const short v = inner_value<RAD, SEP>(in, x + e, y, W, H);
+          invalid |= v < 0;
+          dst[e] = v;
+        }
+      }
+    }
+  } else {
+    for (int i = t; i < 32 * 128; i += kThreads) {
+      const int r = i >> 7, c = i & 127;
+      const short v = inner_value<RAD, SEP>(in, qx + c, qy + r, W, H);
+      invalid |= v < 0;
+      tile[(r + RAD) * kTWP + kCO + c] = v;
+    }
+  }
+  // Halo: RAD rows above and below (corners included), RAD columns left and right.
+  constexpr int NROW = 2 * RAD * TW, NHALO = NROW + 2 * RAD * 32;
+  for (int i = t; i < NHALO; i += kThreads) {
+    int ty, tc;
+    if (i < NROW) {
+      const int r = i / TW;
+      tc = i - r * TW - RAD;
+      ty = r < RAD ? r - RAD : 32 + r - RAD;
+    } else {
+      const int j = i - NROW, r = j / (2 * RAD), q = j - r * 2 * RAD;
+      ty = r;
+      tc = q < RAD ? q - RAD : 128 + q - RAD;
+    }
+    const bool fetch = SEP ? sep_fetch<RAD>(qx, qy, ty, tc, W, H) : tap_valid(RAD, qx, qy, ty, tc, W, H);
+    const short v = fetch ? (short)in[(long long)(qy + ty) * W + qx + tc] : (SEP && RAD == 1 ? 0 : -1);
+    invalid |= v < 0;
+    tile[(ty + RAD) * kTWP + kCO + tc] = v;
+  }
+  return invalid;
+}
+
+__device__ __forceinline__ u2 as_u2(uint32_t v) { return __builtin_bit_cast(u2, v); }
+__device__ __forceinline__ uint32_t as_u32(u2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// Horizontal pass of one LDS row at the thread's columns c0..c0+3 (`row` points at column
+// c0-2): packed sums sum_j t_j * f(v[c + j - RAD]) for columns (c0, c0+1) and (c0+2, c0+3);
+// f(v) = max(v, 0) (numerator) or [v < 0] (invalid indicator).
+template <int RAD, bool IND>
+__device__ __forceinline__ void hpass(const short *row, const u2 (&tt)[5], u2 &p01, u2 &p23) {
+  const uint2 a = *reinterpret_cast<const uint2 *>(row);       // columns c0-2 .. c0+1
+  const uint2 b = *reinterpret_cast<const uint2 *>(row + 4);   // columns c0+2 .. c0+5
+  uint32_t m[4] = {a.x, a.y, b.x, b.y};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (IND) m[k] = as_u32(as_u2(m[k]) >> (u2){15, 15});
+    else m[k] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, m[k]), (s2){0, 0}));
+  }
+  const u2 M0 = as_u2(m[0]), M1 = as_u2(m[1]), M2 = as_u2(m[2]), M3 = as_u2(m[3]);
+  const u2 S0 = as_u2(__builtin_amdgcn_alignbit(m[1], m[0], 16));  // columns c0-1, c0
+  const u2 S1 = as_u2(__builtin_amdgcn_alignbit(m[2], m[1], 16));  // c0+1, c0+2
+  const u2 S2 = as_u2(__builtin_amdgcn_alignbit(m[3], m[2], 16));  // c0+3, c0+4
+  if (RAD == 1) {
+    p01 = tt[0] * S0 + tt[1] * M1 + tt[2] * S1;
+    p23 = tt[0] * S1 + tt[1] * M2 + tt[2] * S2;
+  } else {
+    p01 = tt[0] * M0 + tt[1] * S0 + tt[2] * M1 + tt[3] * S1 + tt[4] * M2;
+    p23 = tt[0] * M1 + tt[1] * S1 + tt[2] * M2 + tt[3] * S2 + tt[4] * M3;
+  }
+}
+
+// Vertical pass: sum_i t_i * hp[i], low and high column.
+template <int KS>
+__device__ __forceinline__ void vpass(const u2 *hp, const int (&t)[5], uint32_t &lo, uint32_t &hi) {
+  lo = hi = 0;
+#pragma unroll
+  for (int i = 0; i < KS; i++) {
+    lo = __builtin_amdgcn_udot2(hp[i], (u2){(unsigned short)t[i], 0}, lo, false);
+    hi = __builtin_amdgcn_udot2(hp[i], (u2){0, (unsigned short)t[i]}, hi, false);
+  }
+}
+
+// Exact (x + s/2) / s for x + s/2 < 2^24, s >= 1 (float estimate, one correction step).
+__device__ __forceinline__ uint32_t div_round(int x, int s) {
+  const int n = x + (s >> 1);
+  int q = (int)((float)n * __builtin_amdgcn_rcpf((float)s));
+  const int r = n - q * s;
+  q += (r >= s) - (r < 0);
+  return (uint32_t)q;
+}
+
+// Separable position-class scale of pixel (x, y) (intra.cl:3281-3285, 3523-3557).
+template <int RAD>
+__device__ __forceinline__ int sep_scale(int x, int y, int W, int H, int full, const int (&cls)[7]) {
+  if (RAD == 1) {
+    const int nb = (y == 0) + (y == H - 1) + (x == 0) + (x == W - 1);
+    return nb >= 2 ? cls[0] : (nb ? cls[1] : full);
+  }
+  const bool otb = y == 0 || y == H - 1, itb = y == 1 || y == H - 2;
+  const bool olr = x == 0 || x == W - 1, ilr = x == 1 || x == W - 2;
+  const bool o_corner = otb && olr, i_corner = itb && ilr;
+  const bool iface = (olr && itb) || (ilr && otb);
+  int sc = full;
+  if (o_corner) sc = cls[2];
+  if (i_corner) sc = cls[3];
+  if (!o_corner && !iface && (otb || olr)) sc = cls[5];
+  if (!i_corner && !iface && (itb || ilr)) sc = cls[6];
+  if (iface) sc = cls[4];
+  return sc;
+}
+
+template <int RAD, bool FLOAT, bool SEP>
+__global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
+  constexpr int KS = 2 * RAD + 1, TH = 32 + 2 * RAD, NR = 8 + 2 * RAD;
+  __shared__ __attribute__((aligned(16))) short tile[TH * kTWP];
   const int qx = 128 * blockIdx.x, qy = 32 * blockIdx.y, f = blockIdx.z;
   const int W = a.width, H = a.height;
   const uint16_t *in = a.in + (size_t)f * W * H;
-  for (int i = threadIdx.x; i < TH * TW; i += blockDim.x) {
-    const int r = i / TW, c = i - r * TW;
-    const int ty = r - RAD, tc = c - RAD, y = qy + ty, x = qx + tc;
-    short v = RAD == 1 ? 0 : -1;  // not fetched: 0 (3 taps) / dropped (5 taps)
-    // Fetched halo cells read the reference's linear index (in range by sep_fetch; it
-    // wraps into the neighbouring row only when W % 128 != 0); interior cells outside
-    // the frame read 0.
-    const bool inner = ty >= 0 && ty < 32 && tc >= 0 && tc < 128;
-    if (sep_fetch<RAD>(qx, qy, ty, tc, W, H))
-      v = !inner ? (short)in[(long long)y * W + x] : (y < H && x < W) ? (short)in[(size_t)y * W + x] : 0;
-    tile[i] = v;
-  }
+  const bool inv_local = stage<RAD, SEP>(tile, in, qx, qy, W, H);
+  const bool irregular = __syncthreads_or(inv_local);  // some cell of the window is invalid
+
   const uint16_t *k2 = RAD == 1 ? c_taps3 + 9 * a.kernel_idx : c_taps5 + 25 * a.kernel_idx;
-  int t[KS];
+  int t[5] = {0, 0, 0, 0, 0};
 #pragma unroll
-  for (int i = 0; i < KS; i++) t[i] = k2[i];  // row 0 of the 2-D kernel
-  __syncthreads();
-  for (int i = threadIdx.x; i < TH * 128; i += blockDim.x) {
-    const int r = i >> 7, c = i & 127;
-    int acc = 0;
+  for (int i = 0; i < KS; i++) t[i] = k2[i];
+  u2 tt[5];
 #pragma unroll
-    for (int d = 0; d < KS; d++) acc += max((int)tile[r * TW + c + d], 0) * t[d];
-    const bool row_ok = RAD == 1 || (qy + r - RAD >= 0 && qy + r - RAD < H);
-    hsum[i] = row_ok ? acc : -1;
-  }
-  __syncthreads();
-  int full, s_corner = 0, s_edge = 0, oc = 0, ic = 0, itf = 0, oe = 0, ie = 0;
-  if (RAD == 1) {
-    full = 4 * t[0] + 4 * t[1] + t[1] * t[1];
-    s_corner = t[0] + 2 * t[1] + t[1] * t[1];
-    s_edge = 2 * t[0] + 3 * t[1] + t[1] * t[1];
-  } else {
-    full = 0;
-    for (int i = 0; i < 5; i++)
-      for (int j = 0; j < 5; j++) {
-        const int v = k2[i * 5 + j];
-        full += v;
-        if (i >= 2 && j >= 2) oc += v;
-        if (i >= 1 && j >= 1) ic += v;
-        if (i >= 1 && j >= 2) itf += v;
-        if (j >= 2) oe += v;
-        if (j >= 1) ie += v;
-      }
-  }
-  uint16_t *out = a.out + (size_t)f * W * H;
-  for (int i = threadIdx.x; i < 128 * 32; i += blockDim.x) {
-    const int ty = i >> 7, tc = i & 127, y = qy + ty, x = qx + tc;
-    if (y >= H || x >= W) continue;
-    int v = 0, sc = full;
+  for (int i = 0; i < 5; i++) tt[i] = (u2){(unsigned short)t[i], (unsigned short)t[i]};
+  int tsum = 0;
 #pragma unroll
-    for (int d = 0; d < KS; d++) {
-      const int h = hsum[(ty + d) * 128 + tc];
-      if (h < 0) sc -= t[d];
-      else v += h * t[d];
-    }
+  for (int i = 0; i < KS; i++) tsum += t[i];
+  const int d = SEP ? 0 : (int)k2[RAD * KS + RAD] - t[RAD] * t[RAD];  // centre excess
+  int full = tsum * tsum + d;
+
+  // Separable class scales: 3 taps {corner, edge}; 5 taps {-, -, outer corner, inner
+  // corner, interface, outer edge, inner edge} (oracle filter_1d_tile3/5).
+  int cls[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (SEP) {
     if (RAD == 1) {
-      const int nb = (y == 0) + (y == H - 1) + (x == 0) + (x == W - 1);
-      sc = nb >= 2 ? s_corner : (nb ? s_edge : full);
+      full = 4 * t[0] + 4 * t[1] + t[1] * t[1];
+      cls[0] = t[0] + 2 * t[1] + t[1] * t[1];
+      cls[1] = 2 * t[0] + 3 * t[1] + t[1] * t[1];
     } else {
-      const bool otb = y == 0 || y == H - 1, itb = y == 1 || y == H - 2;
-      const bool olr = x == 0 || x == W - 1, ilr = x == 1 || x == W - 2;
-      const bool o_corner = otb && olr, i_corner = itb && ilr;
-      const bool iface = (olr && itb) || (ilr && otb);
-      if (o_corner) sc = oc;
-      if (i_corner) sc = ic;
-      if (!o_corner && !iface && (otb || olr)) sc = oe;
-      if (!i_corner && !iface && (itb || ilr)) sc = ie;
-      if (iface) sc = itf;
+      full = 0;
+#pragma unroll
+      for (int i = 0; i < 5; i++)
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+          const int v = k2[i * 5 + j];
+          full += v;
+          if (i >= 2 && j >= 2) cls[2] += v;
+          if (i >= 1 && j >= 1) cls[3] += v;
+          if (i >= 1 && j >= 2) cls[4] += v;
+          if (j >= 2) cls[5] += v;
+          if (j >= 1) cls[6] += v;
+        }
     }
-    int r;
-    if (FLOAT) r = (int)roundf(ref_fdiv((float)v, (float)sc));
-    else r = (v + sc / 2) / sc;
-    out[(size_t)y * W + x] = (uint16_t)r;
+  }
+
+  const int c0 = 4 * (threadIdx.x & 31), r0 = 8 * (threadIdx.x >> 5);
+  const short *rowp = tile + r0 * kTWP + kCO - 2 + c0;
+  u2 h01[NR], h23[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) hpass<RAD, false>(rowp + r * kTWP, tt, h01[r], h23[r]);
+
+  // Uniform scale: every window fully valid (2-D) / no frame-border class (separable).
+  const bool uniform = SEP ? (qx >= 2 && qx + 128 <= W - 2 && qy >= 2 && qy + 32 <= H - 2) : !irregular;
+  u2 n01[NR], n23[NR];
+  if (!SEP && !uniform) {
+#pragma unroll
+    for (int r = 0; r < NR; r++) hpass<RAD, true>(rowp + r * kTWP, tt, n01[r], n23[r]);
+  }
+  const float rf = ref_recip((float)full);
+  const uint32_t magic = (uint32_t)(0x100000000ull / (unsigned)full) + ((0x100000000ull % (unsigned)full) != 0);
+
+  uint16_t *out = a.out + (size_t)f * W * H;
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int y = qy + r0 + r;
+    uint32_t num[4];
+    vpass<KS>(h01 + r, t, num[0], num[1]);
+    vpass<KS>(h23 + r, t, num[2], num[3]);
+    if (!SEP && d != 0) {
+      const uint32_t *cp = reinterpret_cast<const uint32_t *>(rowp + (r + RAD) * kTWP + 2);  // centres c0..c0+3
+      const uint32_t cv0 = cp[0], cv1 = cp[1];
+      num[0] += d * (int)(cv0 & 0xffff);
+      num[1] += d * (int)(cv0 >> 16);
+      num[2] += d * (int)(cv1 & 0xffff);
+      num[3] += d * (int)(cv1 >> 16);
+    }
+    uint32_t res[4];
+    if (uniform) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        if (FLOAT) res[c] = (uint32_t)roundf((float)num[c] * rf);
+        else res[c] = __umulhi(num[c] + (uint32_t)(full >> 1), magic);
+      }
+    } else {
+      uint32_t def[4] = {0, 0, 0, 0};
+      if (!SEP) {
+        vpass<KS>(n01 + r, t, def[0], def[1]);
+        vpass<KS>(n23 + r, t, def[2], def[3]);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int s = SEP ? sep_scale<RAD>(qx + c0 + c, y, W, H, full, cls) : full - (int)def[c];
+        if (FLOAT) res[c] = (uint32_t)roundf((float)num[c] * ref_recip((float)s));
+        else res[c] = div_round((int)num[c], s);
+      }
+    }
+    const int x = qx + c0;
+    if (y >= H || x >= W) continue;
+    uint16_t *o = out + (size_t)y * W + x;
+    if ((W & 3) == 0 && x + 4 <= W) {
+      *reinterpret_cast<uint2 *>(o) = make_uint2(res[0] | (res[1] << 16), res[2] | (res[3] << 16));
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        if (x + c < W) o[c] = (uint16_t)res[c];
+    }
   }
 }
 
@@ -214,15 +348,16 @@ __global__ __launch_bounds__(256) void filter1d_kernel(FilterArgs a) {
 
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s) {
   const dim3 grid((a.width + 127) / 128, (a.height + 31) / 32, a.nframes);
+  const dim3 block(kThreads);
   switch (a.filter) {
-    case 0: hipLaunchKernelGGL((filter1d_kernel<1, false>), grid, dim3(256), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((filter1d_kernel<1, true>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((filter2d_kernel<1, false>), grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((filter2d_kernel<1, true>), grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((filter1d_kernel<2, false>), grid, dim3(256), 0, s, a); break;
-    case 5: hipLaunchKernelGGL((filter1d_kernel<2, true>), grid, dim3(256), 0, s, a); break;
-    case 6: hipLaunchKernelGGL((filter2d_kernel<2, false>), grid, dim3(256), 0, s, a); break;
-    case 7: hipLaunchKernelGGL((filter2d_kernel<2, true>), grid, dim3(256), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((filter_kernel<1, false, true>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((filter_kernel<1, true, true>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((filter_kernel<1, false, false>), grid, block, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((filter_kernel<1, true, false>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((filter_kernel<2, false, true>), grid, block, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((filter_kernel<2, true, true>), grid, block, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((filter_kernel<2, false, false>), grid, block, 0, s, a); break;
+    case 7: hipLaunchKernelGGL((filter_kernel<2, true, false>), grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -203,7 +203,6 @@ WorkLists build_work(int slices, int waves) {
   return wl;
 }
 
-bool filter_supported(int f) { return f >= 0 && f <= 7; }
 bool filter_valid(int f, int k) {
   if (f < 0 || f > 7) return false;
   const bool five = f >= 4;
@@ -292,7 +291,6 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   if (o.max_batch < 1) return fail("max_batch must be >= 1");
   if (o.filter != MIP_FILTER_NONE) {
     if (!filter_valid(o.filter, o.kernel_idx)) return fail("invalid filter %d / kernel_idx %d", o.filter, o.kernel_idx);
-    if (!filter_supported(o.filter)) return fail("filter %d (separable) is not available on the HIP path yet", o.filter);
   }
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -347,7 +345,6 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
                       int filter, int kernel_idx, void *stream) {
   if (!d_in || !d_out || nframes < 1) return fail("bad filter arguments");
   if (!filter_valid(filter, kernel_idx)) return fail("invalid filter %d / kernel_idx %d", filter, kernel_idx);
-  if (!filter_supported(filter)) return fail("filter %d (separable) is not available on the HIP path yet", filter);
   mipgpu::FilterArgs a{d_in, d_out, width, height, nframes, filter, kernel_idx};
   HIP_TRY(mipgpu::launch_filter(a, (hipStream_t)stream));
   return 0;
