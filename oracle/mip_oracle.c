@@ -90,6 +90,16 @@ void mipo_cu_boundaries(const uint16_t *refs, int width, int height, int x, int 
 
 /* --------------------------------------------------------- reduced prediction --- */
 
+/* Clip events of the reduced prediction ([0]: below 0, [1]: above 1023), for tests that
+ * need inputs exercising both clips (mipo_clip_counts). */
+static long long mipo_clips[2];
+
+void mipo_clip_counts(long long *out, int reset) {
+  out[0] = __atomic_load_n(&mipo_clips[0], __ATOMIC_RELAXED);
+  out[1] = __atomic_load_n(&mipo_clips[1], __ATOMIC_RELAXED);
+  if (reset) mipo_clips[0] = mipo_clips[1] = 0;
+}
+
 /* Matrix-vector product of one mode, intra.cl:415-487.  Output stored at the
  * transposed position for transposed modes (intra.cl:402-406, 485). */
 void mipo_reduced_pred(int size_id, int mode, int transposed, const int16_t *red_top,
@@ -119,6 +129,7 @@ void mipo_reduced_pred(int size_id, int mode, int transposed, const int16_t *red
       acc += p[i] * w;
     }
     int v = (acc >> 6) + b0;
+    if (v < 0 || v > 1023) __atomic_fetch_add(&mipo_clips[v > 1023], 1, __ATOMIC_RELAXED);
     v = v < 0 ? 0 : (v > 1023 ? 1023 : v);
     const int pos = transposed ? (j % r) * r + j / r : j;
     pred[pos] = (int16_t)v;

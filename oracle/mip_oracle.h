@@ -62,6 +62,9 @@ void mipo_reduced_pred(int size_id, int mode, int transposed, const int16_t *red
                        const int16_t *red_left, int16_t *pred);
 
 /* Low-pass filters (2-D quarter-CTU kernels and separable kernels). */
+/* Counts of reduced-prediction clip events since the last reset ([0] < 0, [1] > 1023). */
+void mipo_clip_counts(long long *out, int reset);
+
 int mipo_filter_frame(const uint16_t *in, uint16_t *out, int width, int height,
                       int filter, int kernel_idx);
 

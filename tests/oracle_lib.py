@@ -34,6 +34,7 @@ def lib():
         L.mipo_synth_frame.argtypes = [u16p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
         L.mipo_num_ctus.argtypes = [ctypes.c_int, ctypes.c_int]
         L.mipo_num_ctus.restype = ctypes.c_int
+        L.mipo_clip_counts.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -55,6 +56,13 @@ def search(orig, refs=None, ctus=None, want_sad_satd=False, nthreads=0):
     satd = np.zeros_like(cost) if want_sad_satd else None
     lib().mipo_search_ctus(orig, refs, w, h, c0, c1, _ptr(cost), _ptr(sad), _ptr(satd), nthreads)
     return (cost, sad, satd) if want_sad_satd else cost
+
+
+def clip_counts(reset=True):
+    """(below 0, above 1023) clip events of the oracle's reduced predictions since the last reset."""
+    out = np.zeros(2, np.int64)
+    lib().mipo_clip_counts(out.ctypes.data_as(ctypes.c_void_p), int(reset))
+    return int(out[0]), int(out[1])
 
 
 def filter_frame(frame, filter_name, kernel_idx):

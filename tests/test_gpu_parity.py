@@ -120,3 +120,36 @@ def test_errors_are_loud(gpu_available):
         MipEngine(128, 64, filter="filterFrame_2d_int_quarterCtu", kernel_idx=7)
     with pytest.raises(MipError):
         filter_index("filterFrame_2d_float")  # not whitelisted
+
+
+def _extreme(pattern, w, h):
+    y, x = np.mgrid[0:h, 0:w]
+    if pattern == "checker1":
+        return np.where((x + y) % 2, 1023, 0)
+    if pattern == "checker4":
+        return np.where((x // 4 + y // 4) % 2, 1023, 0)
+    if pattern == "stripes":
+        return np.where((x // 2) % 2, 1023, 0)
+    if pattern == "binary_noise":
+        return np.random.default_rng(7).integers(0, 2, (h, w)) * 1023
+    if pattern == "lattice8":  # dark frame, bright lines every 8 samples
+        return np.where((x % 8 == 7) | (y % 8 == 5), 1023, 0)
+    return np.full((h, w), 1023 if pattern == "white" else 0)
+
+
+@pytest.mark.parametrize("pattern", ["checker1", "checker4", "stripes", "binary_noise", "lattice8", "white", "black"])
+def test_extreme_content_clipping(gpu_available, pattern):
+    """0/1023 patterns drive the unclipped MIP predictions far outside [0, 1023] (both
+    clipping directions of intra.cl:481-482 and the saturating conversion in phase A)."""
+    w, h = 192, 136
+    frame = _extreme(pattern, w, h).astype(np.uint16)
+    with MipEngine(w, h, want_sad_satd=True) as eng:
+        out = eng.search(frame, sad_satd=True)
+    O.clip_counts(reset=True)
+    oc, osad, osatd = O.search(frame, want_sad_satd=True)
+    low, high = O.clip_counts()
+    if pattern not in ("white", "black"):
+        assert low > 0 and high > 0, (low, high)
+    assert np.array_equal(out["cost"][0], oc)
+    assert np.array_equal(out["sad"][0], osad)
+    assert np.array_equal(out["satd"][0], osatd)

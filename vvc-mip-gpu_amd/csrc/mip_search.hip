@@ -259,13 +259,18 @@ template <int R>
 struct Red {
   const uint32_t *p;
   int k0;
-  __device__ __forceinline__ s2 operator()(int k, int kx) const { return as_s2(p[(k + k0) * R + kx]); }
+  // phase A stores floor(D) saturated at 0 only; the clip to 1023 is applied here, to
+  // both modes of a pair at once
+  static __device__ __forceinline__ s2 clip(uint32_t v) {
+    return __builtin_bit_cast(s2, __builtin_elementwise_min(__builtin_bit_cast(u2, v), (u2){1023, 1023}));
+  }
+  __device__ __forceinline__ s2 operator()(int k, int kx) const { return clip(p[(k + k0) * R + kx]); }
   __device__ __forceinline__ void row4(int k, int kx, s2 (&out)[4]) const {  // kx % 4 == 0
     const uint4 v = *reinterpret_cast<const uint4 *>(p + (k + k0) * R + kx);
-    out[0] = as_s2(v.x);
-    out[1] = as_s2(v.y);
-    out[2] = as_s2(v.z);
-    out[3] = as_s2(v.w);
+    out[0] = clip(v.x);
+    out[1] = clip(v.y);
+    out[2] = clip(v.z);
+    out[3] = clip(v.w);
   }
 };
 
@@ -434,12 +439,17 @@ struct Ctx {
   int fx0, fy0;               // quadrant origin in the frame
 };
 
+// floor(f) for f >= 0, 0 for f < 0: v_cvt_u32_f32 saturates out-of-range inputs.
+__device__ __forceinline__ uint32_t floor_sat(float f) { return (uint32_t)f; }
+
 // Phase A for mode pair q: reduced predictions of every CU of the task,
 //   D[j][n] = C[j] + sum_k A[j][k] B[k][n]     (16x16x16 f16 MFMA, f32 accumulate, exact)
 // rows j = MIP matrix outputs, columns n = (CU 8*cs + n/2, mode 2q + n%2), K = the 8 inputs
 // of mode 2q (k < 8) and of mode 2q+1 (k >= 8), block-diagonal.  floor(D) clipped to
 // [0, 1023] equals the reference's clamp(((offset + sum p*w) >> 6) + b0) (intra.cl:449-482;
-// coefficient restatement in mip_kernels.h).  Results go to scratch[pos][slot] (16-bit
+// coefficient restatement in mip_kernels.h); phase A stores floor(D) saturated at 0 (D is
+// the unclipped sample, |D| <= 8 * 1023 * 127 / 64 + 1023 < 2^16) and Red applies the upper
+// clip to packed pairs on read.  Results go to scratch[pos][slot] (16-bit
 // halves = modes), pos = stored position (transposed modes store output j at (j%R, j/R),
 // intra.cl:402-406, 485).  CHUNKED classes produce reduced rows [4*chunk, 4*chunk + 4).
 template <int W, int H, bool TR>
@@ -496,7 +506,7 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
         uint8_t *dst = lane_dst + (pofs + 8 * cs * G::PITCH) * 4;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          const uint32_t v = (uint32_t)__builtin_amdgcn_fmed3f(d[i], 0.0f, 1023.5f);  // floor + clip
+          const uint32_t v = floor_sat(d[i]);  // < 2^16; the upper clip is applied by Red
           *reinterpret_cast<uint16_t *>(dst + i * PSTEP * 4) = (uint16_t)v;
         }
       }
