@@ -118,7 +118,7 @@ def filter_section(eng_cls, frames, W, H, B, stream, dev, steps, pmc):
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     alg = 2 * 2 * W * H * B
-    res = {"kernel": "filter2d_kernel<5x5, float>", "filter": name, "kernel_idx": kidx, "bound": "hbm",
+    res = {"kernel": "filter_kernel<2, true, false>", "filter": name, "kernel_idx": kidx, "bound": "hbm",
            "kernel_ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": alg,
            "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -236,8 +236,16 @@ template <int RAD, bool FLOAT, bool SEP>
 __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
   constexpr int KS = 2 * RAD + 1, TH = 32 + 2 * RAD, NR = 8 + 2 * RAD;
   __shared__ __attribute__((aligned(16))) short tile[TH * kTWP];
-  const int qx = 128 * blockIdx.x, qy = 32 * blockIdx.y, f = blockIdx.z;
   const int W = a.width, H = a.height;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so workgroup b
+  // takes tile (b % 8) * per + b / 8 -- each XCD walks a contiguous band of tiles and the
+  // halo rows / columns it shares with its neighbours are fetched into its own L2.
+  const int tiles_x = (W + 127) / 128, tiles_y = (H + 31) / 32, per_frame = tiles_x * tiles_y;
+  const int total = per_frame * a.nframes, per = (total + 7) / 8;
+  const int tid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (tid >= total) return;
+  const int f = tid / per_frame, tr = tid - f * per_frame, ty = tr / tiles_x;
+  const int qx = 128 * (tr - ty * tiles_x), qy = 32 * ty;
   const uint16_t *in = a.in + (size_t)f * W * H;
   const bool inv_local = stage<RAD, SEP>(tile, in, qx, qy, W, H);
   const bool irregular = __syncthreads_or(inv_local);  // some cell of the window is invalid
@@ -347,7 +355,9 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
 }  // namespace
 
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s) {
-  const dim3 grid((a.width + 127) / 128, (a.height + 31) / 32, a.nframes);
+  const long long total = (long long)((a.width + 127) / 128) * ((a.height + 31) / 32) * a.nframes;
+  if (total > (1LL << 30)) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((total + 7) / 8 * 8));
   const dim3 block(kThreads);
   switch (a.filter) {
     case 0: hipLaunchKernelGGL((filter_kernel<1, false, true>), grid, block, 0, s, a); break;
