@@ -7,7 +7,7 @@ from mipgpu import MipEngine, layout
 fx = G.load(sys.argv[1] if len(sys.argv) > 1 else 'small_alt_2d_float3'); c = fx['config']; frames = G.inputs(fx)
 with MipEngine(c['width'], c['height'], filter=c['filter'], kernel_idx=c['kernel_idx'], max_batch=c['frames']) as eng:
     out = eng.search(frames)
-refs = O.filter_frame(frames[0], c['filter'], c['kernel_idx'])
+refs = O.filter_frame(frames[0], c['filter'], c['kernel_idx']) if c['filter'] else None
 oc = O.search(frames[0], refs)
 g = out['cost'][0]
 bad = np.nonzero(g != oc)[0]
