@@ -153,3 +153,24 @@ def test_extreme_content_clipping(gpu_available, pattern):
     assert np.array_equal(out["cost"][0], oc)
     assert np.array_equal(out["sad"][0], osad)
     assert np.array_equal(out["satd"][0], osatd)
+
+
+def test_8k_alt_int_sampled_ctus(gpu_available):
+    """BASELINE configs[4] geometry: 7680x4320 with alternative references
+    (filterFrame_2d_int_quarterCtu).  The whole filtered frame and the cost rows of CTUs at
+    the corners, the middle and the partial bottom row are checked against the oracle (the
+    reference itself overflows its int32 reduced-prediction index at 8K: 2040 CTUs x
+    2 231 296 entries > 2^31, intra.cl:519-537)."""
+    w, h, filt = 7680, 4320, "filterFrame_2d_int_quarterCtu"
+    frame = synth_frame(w, h, 0x8E, 1)
+    with MipEngine(w, h, filter=filt, kernel_idx=0) as eng:
+        out = eng.search(frame)
+        got_refs = eng.filter_frames(frame, filt, 0)[0]
+    refs = O.filter_frame(frame, filt, 0)
+    assert np.array_equal(got_refs, refs)
+    n = layout.num_ctus(w, h)
+    cost = out["cost"][0]
+    for c in (0, 59, n // 2, n - 60, n - 1):
+        oc = O.search(frame, refs, ctus=(c, c + 1))
+        sl = slice(c * layout.COSTS_PER_CTU, (c + 1) * layout.COSTS_PER_CTU)
+        assert np.array_equal(cost[sl], oc[sl]), c
