@@ -596,6 +596,8 @@ void mipo_synth_frame(uint16_t *out, int width, int height, uint64_t seed, int k
       int v;
       if (kind == 1) {
         v = (int)(h & 1023);
+      } else if (kind == 2) {
+        v = (int)(h % 3);
       } else {
         const uint64_t hb = splitmix64(seed ^ ((uint64_t)(y >> 5) << 32) ^ (uint64_t)(x >> 5));
         const int ramp = ((x * 3 + y * 5) % 512);

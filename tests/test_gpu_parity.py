@@ -65,10 +65,14 @@ def test_full_size_configs_vs_reference(gpu_available, name):
 @pytest.mark.parametrize("filt,nk", FILTERS)
 def test_filters_vs_oracle(gpu_available, filt, nk):
     frame = synth_frame(392, 136, 0x51, 1)  # partial tiles on both axes
+    # near-black samples: quotients around 1/2 (sum == scale/2 is the case where the
+    # reference's fp32 division can fall just below the tie)
+    dark = np.random.default_rng(5).integers(0, 3, (136, 392)).astype(np.uint16)
     with MipEngine(392, 136) as eng:
         for k in range(nk):
-            got = eng.filter_frames(frame, filt, k)[0]
-            assert np.array_equal(got, O.filter_frame(frame, filt, k)), (filt, k)
+            for fr in (frame, dark):
+                got = eng.filter_frames(fr, filt, k)[0]
+                assert np.array_equal(got, O.filter_frame(fr, filt, k)), (filt, k)
 
 
 @pytest.mark.parametrize("w,h,kind", [(136, 72, 0), (8, 8, 1), (132, 260, 1), (128, 4, 0), (640, 384, 1)])

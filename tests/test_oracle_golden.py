@@ -17,7 +17,7 @@ def _refs(fx, frames, f):
 
 
 def test_synth_generators_agree():
-    for kind in (0, 1):
+    for kind in (0, 1, 2):
         assert (O.synth(136, 72, 0xABC, kind) == synth_frame(136, 72, 0xABC, kind)).all()
 
 

@@ -57,6 +57,12 @@ CONFIGS = {
     # float filters with scales whose fp32 quotient ties depend on the reference's division
     "small_alt_2d_float3_k2": (384, 256, 1, 0, 0x3A6, "filterFrame_2d_float_quarterCtu", 2, False, [0, 4]),
     "small_alt_2d_float3_k4": (256, 264, 1, 1, 0x3A7, "filterFrame_2d_float_quarterCtu", 4, False, [1]),
+    # near-black frames: quotients around 1/2, where the reference's fp32 division decides
+    "small_dark_2d_float3_k2": (256, 136, 1, 2, 0x3D0, "filterFrame_2d_float_quarterCtu", 2, False, [0]),
+    "small_dark_2d_float3_k0": (256, 136, 1, 2, 0x3D1, "filterFrame_2d_float_quarterCtu", 0, False, [0]),
+    "small_dark_1d_float_k4": (256, 136, 1, 2, 0x3D2, "filterFrame_1d_float", 4, False, [0]),
+    "small_dark_2d_float5_k1": (256, 136, 1, 2, 0x3D3, "filterFrame_2d_float_5x5_quarterCtu", 1, False, [0]),
+    "small_dark_1d_float5_k1": (256, 136, 1, 2, 0x3D4, "filterFrame_1d_float_5x5", 1, False, [0]),
 }
 
 

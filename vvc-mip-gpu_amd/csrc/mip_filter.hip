@@ -34,7 +34,7 @@ typedef short s2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u2 __attribute__((ext_vector_type(2)));
 
 constexpr int kThreads = 128;  // per tile: thread t owns columns 4(t&31).. +3, rows 8(t>>5).. +7
-constexpr int kCO = 10;        // LDS column of tile column 0 (tile column c0-2 is 8-byte aligned)
+constexpr int kCO = 8;         // LDS column of tile column 0 (interior rows 16-byte aligned)
 constexpr int kTWP = 144;      // LDS row pitch in samples
 
 __constant__ uint16_t c_taps3[5 * 9] = MIP_TAPS_3x3;
@@ -46,11 +46,19 @@ __device__ __forceinline__ float ref_recip(float s) {
                                  -__builtin_amdgcn_frexp_expf(s));
 }
 
+// round(x) for x >= 0 (round half up == round half away from zero): v_cvt_rpi_i32_f32
+// computes floor(x + 0.5) without rounding the sum.
+__device__ __forceinline__ uint32_t round_pos(float x) {
+  int r;
+  asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return (uint32_t)r;
+}
+
 // Validity of tile cell (ty, tc) of the tile at (qx, qy): 3x3 gates intra.cl:2903-2966,
 // 5x5 gates intra.cl:3096-3189.  Interior cells: inside the frame.
 __device__ __forceinline__ bool tap_valid(int rad, int qx, int qy, int ty, int tc, int W, int H) {
-  const long long WH = (long long)W * H;
-  const long long g = (long long)(qy + ty) * W + qx + tc;
+  const int WH = W * H;                            // < 2^31 (launch_filter)
+  const int g = __mul24(qy + ty, W) + qx + tc;     // linear index, as the reference computes it
   const bool top = ty < 0, bot = ty >= 32, lft = tc < 0, rgt = tc >= 128;
   if (!top && !bot && !lft && !rgt) return qy + ty < H && qx + tc < W;
   if ((top || bot) && (lft || rgt)) {
@@ -70,16 +78,16 @@ __device__ __forceinline__ bool tap_valid(int rad, int qx, int qy, int ty, int t
 // 3 taps, 3566-3640 for 5 taps)?
 template <int RAD>
 __device__ __forceinline__ bool sep_fetch(int qx, int qy, int ty, int tc, int W, int H) {
-  const long long WH = (long long)W * H;
-  const long long g = (long long)(qy + ty) * W + qx + tc;
+  const int WH = W * H;
+  const int g = __mul24(qy + ty, W) + qx + tc;
   const bool top = ty < 0, bot = ty >= 32, lft = tc < 0, rgt = tc >= 128;
   if (RAD == 1) {
     if ((top || bot) && (lft || rgt)) {
-      const long long b = (long long)qy * W + qx;
+      const int b = __mul24(qy, W) + qx;
       if (top && lft) return b - W - 1 > 0 && qx > 0 && qy > 0;
       if (top) return b - W + 128 > 0 && qx + 128 < W - 1 && qy > 0;
-      if (lft) return b + 32LL * W - 1 < WH && qx > 0 && qy + 32 < H - 1;
-      return b + 32LL * W + 128 < WH && qx + 128 < W - 1 && qy + 32 < H - 1;
+      if (lft) return b + 32 * W - 1 < WH && qx > 0 && qy + 32 < H - 1;
+      return b + 32 * W + 128 < WH && qx + 128 < W - 1 && qy + 32 < H - 1;
     }
     if (top || bot) return g > 0 && g < WH;
     return g > 0 && g < WH && (lft ? qx > 0 : qx + 129 < W - 1);
@@ -119,12 +127,7 @@ __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, i
       const int y = qy + r, x = qx + 8 * k;
       short *dst = tile + (r + RAD) * kTWP + kCO + 8 * k;
       if (y < H && x + 8 <= W) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(in + (size_t)y * W + x);
-        uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);  // 4-byte aligned (kCO even)
-        d32[0] = v.x;
-        d32[1] = v.y;
-        d32[2] = v.z;
-        d32[3] = v.w;
+        *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<const uint4 *>(in + (size_t)y * W + x);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; e++) {
@@ -171,9 +174,8 @@ __device__ __forceinline__ uint32_t as_u32(u2 v) { return __builtin_bit_cast(uin
 // f(v) = max(v, 0) (numerator) or [v < 0] (invalid indicator).
 template <int RAD, bool IND>
 __device__ __forceinline__ void hpass(const short *row, const u2 (&tt)[5], u2 &p01, u2 &p23) {
-  const uint2 a = *reinterpret_cast<const uint2 *>(row);       // columns c0-2 .. c0+1
-  const uint2 b = *reinterpret_cast<const uint2 *>(row + 4);   // columns c0+2 .. c0+5
-  uint32_t m[4] = {a.x, a.y, b.x, b.y};
+  const uint32_t *row32 = reinterpret_cast<const uint32_t *>(row);  // 4-byte aligned
+  uint32_t m[4] = {row32[0], row32[1], row32[2], row32[3]};        // columns c0-2 .. c0+5
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     if (IND) m[k] = as_u32(as_u2(m[k]) >> (u2){15, 15});
@@ -301,6 +303,7 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
 #pragma unroll
     for (int r = 0; r < NR; r++) hpass<RAD, true>(rowp + r * kTWP, tt, n01[r], n23[r]);
   }
+  const bool narrow = tsum * tsum * 1023 < 65536;  // separable part of the sum fits 16 bits
   const float rf = ref_recip((float)full);
   const uint32_t magic = (uint32_t)(0x100000000ull / (unsigned)full) + ((0x100000000ull % (unsigned)full) != 0);
 
@@ -309,8 +312,21 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
   for (int r = 0; r < 8; r++) {
     const int y = qy + r0 + r;
     uint32_t num[4];
-    vpass<KS>(h01 + r, t, num[0], num[1]);
-    vpass<KS>(h23 + r, t, num[2], num[3]);
+    if (narrow) {  // sums < 2^16: packed vertical pass
+      u2 v01 = tt[0] * h01[r], v23 = tt[0] * h23[r];
+#pragma unroll
+      for (int i = 1; i < KS; i++) {
+        v01 += tt[i] * h01[r + i];
+        v23 += tt[i] * h23[r + i];
+      }
+      num[0] = as_u32(v01) & 0xffff;
+      num[1] = as_u32(v01) >> 16;
+      num[2] = as_u32(v23) & 0xffff;
+      num[3] = as_u32(v23) >> 16;
+    } else {
+      vpass<KS>(h01 + r, t, num[0], num[1]);
+      vpass<KS>(h23 + r, t, num[2], num[3]);
+    }
     if (!SEP && d != 0) {
       const uint32_t *cp = reinterpret_cast<const uint32_t *>(rowp + (r + RAD) * kTWP + 2);  // centres c0..c0+3
       const uint32_t cv0 = cp[0], cv1 = cp[1];
@@ -323,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
     if (uniform) {
 #pragma unroll
       for (int c = 0; c < 4; c++) {
-        if (FLOAT) res[c] = (uint32_t)roundf((float)num[c] * rf);
+        if (FLOAT) res[c] = round_pos((float)num[c] * rf);
         else res[c] = __umulhi(num[c] + (uint32_t)(full >> 1), magic);
       }
     } else {
@@ -335,7 +351,7 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         const int s = SEP ? sep_scale<RAD>(qx + c0 + c, y, W, H, full, cls) : full - (int)def[c];
-        if (FLOAT) res[c] = (uint32_t)roundf((float)num[c] * ref_recip((float)s));
+        if (FLOAT) res[c] = round_pos((float)num[c] * ref_recip((float)s));
         else res[c] = div_round((int)num[c], s);
       }
     }
@@ -356,7 +372,9 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
 
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s) {
   const long long total = (long long)((a.width + 127) / 128) * ((a.height + 31) / 32) * a.nframes;
-  if (total > (1LL << 30)) return hipErrorInvalidValue;
+  if (total > (1LL << 30) || (long long)(a.width + 256) * (a.height + 64) >= (1LL << 31) || a.width >= (1 << 22) ||
+      a.height >= (1 << 22))
+    return hipErrorInvalidValue;  // 32-bit / 24-bit index arithmetic in the gates
   const dim3 grid((unsigned)((total + 7) / 8 * 8));
   const dim3 block(kThreads);
   switch (a.filter) {

@@ -16,13 +16,16 @@ def _splitmix64(z: np.ndarray) -> np.ndarray:
 
 
 def synth_frame(width: int, height: int, seed: int, kind: int = 0) -> np.ndarray:
-    """kind 0: structured (ramps + texture + block DC + noise); kind 1: uniform noise."""
+    """kind 0: structured (ramps + texture + block DC + noise); kind 1: uniform noise;
+    kind 2: near-black noise in {0, 1, 2} (filter quotients around 1/2)."""
     y, x = np.meshgrid(np.arange(height, dtype=np.uint64), np.arange(width, dtype=np.uint64), indexing="ij")
     with np.errstate(over="ignore"):
         s = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
         h = _splitmix64(s * np.uint64(0x100000001B3) + y * np.uint64(width) + x)
     if kind == 1:
         return (h & np.uint64(1023)).astype(np.uint16)
+    if kind == 2:
+        return (h % np.uint64(3)).astype(np.uint16)
     hb = _splitmix64(s ^ ((y >> np.uint64(5)) << np.uint64(32)) ^ (x >> np.uint64(5)))
     xi, yi = x.astype(np.int64), y.astype(np.int64)
     ramp = (xi * 3 + yi * 5) % 512
