@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MIPGPU_ABI_VERSION 1
+#define MIPGPU_ABI_VERSION 2
 #define MIP_COSTS_PER_CTU_ABI 97840
 #define MIP_CUS_PER_CTU_ABI 5380
 #define MIP_COST_UNAVAILABLE 0x7fffffff
@@ -84,7 +84,8 @@ int mip_cu_position(int shape, int cu, int *x, int *y);
 int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int filter,
                       int kernel_idx, uint16_t *out);
 
-/* Full MIP search of `nframes` (<= max_batch) host frames: H2D, [filter], search, D2H.
+/* Full MIP search of `nframes` host frames: H2D, [filter], search, D2H, in chunks of
+ * max_batch/2 frames whose transfers overlap the next chunk's search (two streams).
  * Replaces the per-frame loop main.cpp:678-1241 + readMemobjsIntoArray_Distortion.
  * refs_or_null: caller-provided reference-sample frames (alternative samples computed
  * elsewhere); NULL = originals, or the engine's filter when opts.filter != NONE.
@@ -114,6 +115,13 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
  * device time per launch in milliseconds (HIP events on that stream), or <0. */
 double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
                               int nframes, int32_t *d_costs, int reps);
+
+/* Page-locked host memory (hipHostMalloc): host buffers for mip_search_frames /
+ * mip_filter_frames allocated here are transferred by DMA at full PCIe rate (pageable
+ * buffers are staged through the runtime -- the cost table is 52.8 MB per 1080p frame).
+ * Replaces the reference's malloc'd return_minSadHad etc. (main.cpp:656-668). */
+int mip_host_alloc(size_t bytes, void **out);
+int mip_host_free(void *p);
 
 /* Last error message of the calling thread ("" if none). */
 const char *mip_last_error(void);

@@ -152,12 +152,30 @@ int report_parameters(const Options &o, bool alt) {
   return errors;
 }
 
+// Page-locked host buffer (mip_host_alloc): the engine's transfers run at DMA rate.
+template <class T>
+struct Pinned {
+  T *p = nullptr;
+  size_t n = 0;
+  bool alloc(size_t count) {
+    void *v = nullptr;
+    if (mip_host_alloc(count * sizeof(T), &v) != 0) return false;
+    p = static_cast<T *>(v);
+    n = count;
+    return true;
+  }
+  ~Pinned() { mip_host_free(p); }
+  T *data() { return p; }
+  bool empty() const { return n == 0; }
+  T &operator[](size_t i) { return p[i]; }
+};
+
 // Fast CSV reader (main.cpp:364-384 format).
-bool read_frames(const std::string &path, int W, int H, int n, std::vector<uint16_t> &out) {
+bool read_frames(const std::string &path, int W, int H, int n, uint16_t *out) {
   std::ifstream f(path, std::ios::binary);
   if (!f) return false;
   std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  out.assign((size_t)W * H * n, 0);
+  memset(out, 0, (size_t)W * H * n * sizeof(uint16_t));
   const char *p = data.c_str(), *end = p + data.size();
   for (size_t row = 0; row < (size_t)H * n; row++) {
     for (int x = 0; x < W; x++) {
@@ -262,8 +280,12 @@ int main(int argc, char **argv) {
     std::cout << "  [!] ERROR: Input resolution \"" << o.resolution << "\" not set properly" << std::endl;
     return 0;
   }
-  std::vector<uint16_t> frames;
-  if (!read_frames(o.input, W, H, o.frames, frames)) {
+  Pinned<uint16_t> frames;
+  if (!frames.alloc((size_t)W * H * std::max(1, o.frames))) {
+    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
+    return 1;
+  }
+  if (!read_frames(o.input, W, H, o.frames, frames.data())) {
     perror("error while opening samples files");
     return 1;
   }
@@ -280,10 +302,16 @@ int main(int argc, char **argv) {
     return 1;
   }
   const size_t cpf = (size_t)nctus * MIP_COSTS_PER_CTU_ABI, upf = (size_t)nctus * MIP_CUS_PER_CTU_ABI;
-  std::vector<int32_t> cost(cpf * o.frames), sad, satd, best_cost;
-  std::vector<uint8_t> best;
-  if (o.sad_satd) sad.resize(cost.size()), satd.resize(cost.size());
-  if (!o.best_modes.empty()) best.resize(upf * o.frames), best_cost.resize(upf * o.frames);
+  Pinned<int32_t> cost, sad, satd, best_cost;
+  Pinned<uint8_t> best;
+  bool ok = cost.alloc(cpf * o.frames);
+  if (o.sad_satd) ok = ok && sad.alloc(cpf * o.frames) && satd.alloc(cpf * o.frames);
+  if (!o.best_modes.empty()) ok = ok && best.alloc(upf * o.frames) && best_cost.alloc(upf * o.frames);
+  if (!ok) {
+    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
+    mip_engine_destroy(e);
+    return 1;
+  }
 
   const auto t0 = std::chrono::steady_clock::now();  // save_startTime, main.cpp:568
   const int rc = mip_search_frames(e, frames.data(), nullptr, o.frames, cost.data(),

@@ -214,7 +214,7 @@ bool filter_valid(int f, int k) {
 struct mip_engine {
   int device = 0, width = 0, height = 0, nctus = 0, ctu_cols = 0;
   mip_opts opts{};
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr, stream2 = nullptr;  // host API: two halves of the batch in flight
   uint16_t *d_frames = nullptr, *d_refs = nullptr;
   int32_t *d_costs = nullptr, *d_sad = nullptr, *d_satd = nullptr, *d_best_cost = nullptr;
   uint8_t *d_best = nullptr;
@@ -271,11 +271,13 @@ int mip_engine_destroy(mip_engine *e) {
   if (!e) return 0;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tasks,
                   (void *)e->d_jobs, (void *)e->d_lists, (void *)e->d_tables})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->stream2) (void)hipStreamDestroy(e->stream2);
   delete e;
   return 0;
 }
@@ -312,7 +314,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     hipError_t _e = hipMalloc((void **)&(ptr), (bytes));                                \
     if (_e != hipSuccess) return cleanup(fail("hipMalloc(%zu): %s", (size_t)(bytes), hipGetErrorString(_e))); \
   } while (0)
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail("hipStreamCreate failed"));
   ALLOC(e->d_frames, fs * nb * 2);
   if (o.filter != MIP_FILTER_NONE) ALLOC(e->d_refs, fs * nb * 2);
@@ -434,33 +437,60 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
                       int32_t *satd_out) {
   if (!e || !frames || nframes < 1) return fail("bad search arguments");
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
-  if (refs_or_null && e->opts.filter == MIP_FILTER_NONE && !e->d_refs) {
-    const size_t fs = (size_t)e->width * e->height;
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
-  }
   HIP_TRY(hipSetDevice(e->device));
   const size_t fs = (size_t)e->width * e->height;
+  if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
+    HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
   const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU;
-  for (int f0 = 0; f0 < nframes; f0 += e->opts.max_batch) {
-    const int nb = std::min(e->opts.max_batch, nframes - f0);
-    HIP_TRY(hipMemcpyAsync(e->d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, e->stream));
+  // Chunks of `sb` frames alternate between the two halves of the engine buffers, each half
+  // with its own stream (H2D, [filter], search, D2H in order), so the transfers of one chunk
+  // overlap the search of the next.  Transfers run at DMA rate from page-locked host
+  // memory (mip_host_alloc); pageable buffers are staged by the runtime.
+  const int sb = e->opts.max_batch >= 2 ? e->opts.max_batch / 2 : 1;
+  for (int f0 = 0, k = 0; f0 < nframes; f0 += sb, k++) {
+    const int nb = std::min(sb, nframes - f0);
+    const int h = e->opts.max_batch >= 2 ? (k & 1) : 0;
+    const hipStream_t st = h ? e->stream2 : e->stream;
+    const size_t fo = (size_t)h * sb;  // first engine frame slot of this half
+    uint16_t *d_frames = e->d_frames + fo * fs;
+    HIP_TRY(hipMemcpyAsync(d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, st));
     const uint16_t *d_refs = nullptr;
     if (refs_or_null) {
-      HIP_TRY(hipMemcpyAsync(e->d_refs, refs_or_null + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, e->stream));
-      d_refs = e->d_refs;
+      HIP_TRY(hipMemcpyAsync(e->d_refs + fo * fs, refs_or_null + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, st));
+      d_refs = e->d_refs + fo * fs;
+    } else if (e->opts.filter != MIP_FILTER_NONE) {
+      if (mip_filter_device(d_frames, e->d_refs + fo * fs, e->width, e->height, nb, e->opts.filter,
+                            e->opts.kernel_idx, st) != 0)
+        return -1;
+      d_refs = e->d_refs + fo * fs;
     }
-    if (search_device_impl(e, e->d_frames, d_refs, nb, e->d_costs, sad_out ? e->d_sad : nullptr,
-                           satd_out ? e->d_satd : nullptr, best_mode_out ? e->d_best : nullptr,
-                           best_cost_out ? e->d_best_cost : nullptr, e->stream) != 0)
+    int32_t *d_costs = e->d_costs + fo * cpf;
+    int32_t *d_sad = sad_out ? e->d_sad + fo * cpf : nullptr, *d_satd = satd_out ? e->d_satd + fo * cpf : nullptr;
+    uint8_t *d_best = best_mode_out ? e->d_best + fo * upf : nullptr;
+    int32_t *d_best_cost = best_cost_out ? e->d_best_cost + fo * upf : nullptr;
+    if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, st) != 0)
       return -1;
-    if (costs_out) HIP_TRY(hipMemcpyAsync(costs_out + f0 * cpf, e->d_costs, nb * cpf * 4, hipMemcpyDeviceToHost, e->stream));
-    if (sad_out) HIP_TRY(hipMemcpyAsync(sad_out + f0 * cpf, e->d_sad, nb * cpf * 4, hipMemcpyDeviceToHost, e->stream));
-    if (satd_out) HIP_TRY(hipMemcpyAsync(satd_out + f0 * cpf, e->d_satd, nb * cpf * 4, hipMemcpyDeviceToHost, e->stream));
-    if (best_mode_out) HIP_TRY(hipMemcpyAsync(best_mode_out + f0 * upf, e->d_best, nb * upf, hipMemcpyDeviceToHost, e->stream));
-    if (best_cost_out) HIP_TRY(hipMemcpyAsync(best_cost_out + f0 * upf, e->d_best_cost, nb * upf * 4, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (costs_out) HIP_TRY(hipMemcpyAsync(costs_out + f0 * cpf, d_costs, nb * cpf * 4, hipMemcpyDeviceToHost, st));
+    if (sad_out) HIP_TRY(hipMemcpyAsync(sad_out + f0 * cpf, d_sad, nb * cpf * 4, hipMemcpyDeviceToHost, st));
+    if (satd_out) HIP_TRY(hipMemcpyAsync(satd_out + f0 * cpf, d_satd, nb * cpf * 4, hipMemcpyDeviceToHost, st));
+    if (best_mode_out) HIP_TRY(hipMemcpyAsync(best_mode_out + f0 * upf, d_best, nb * upf, hipMemcpyDeviceToHost, st));
+    if (best_cost_out)
+      HIP_TRY(hipMemcpyAsync(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, hipMemcpyDeviceToHost, st));
   }
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream2));
+  return 0;
+}
+
+int mip_host_alloc(size_t bytes, void **out) {
+  if (!out) return fail("out is NULL");
+  *out = nullptr;
+  HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return 0;
+}
+
+int mip_host_free(void *p) {
+  if (p) HIP_TRY(hipHostFree(p));
   return 0;
 }
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -84,6 +85,8 @@ def library():
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
         "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
+        "mip_host_alloc": (ip, [ctypes.c_size_t, ctypes.POINTER(vp)]),
+        "mip_host_free": (ip, [vp]),
         "mip_last_error": (ctypes.c_char_p, []),
         "mip_abi_version": (ip, []),
     }
@@ -106,6 +109,18 @@ def _ptr(a):
     if isinstance(a, np.ndarray):
         return a.ctypes.data
     return a.data_ptr()  # torch tensor
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """Uninitialised numpy array in page-locked host memory (mip_host_alloc); transfers
+    to / from it run at DMA rate.  The memory is released with the last view of it."""
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    p = ctypes.c_void_p()
+    _check(library().mip_host_alloc(max(1, count * dt.itemsize), ctypes.byref(p)))
+    buf = (ctypes.c_byte * max(1, count * dt.itemsize)).from_address(p.value)
+    weakref.finalize(buf, library().mip_host_free, ctypes.c_void_p(p.value))
+    return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
 
 
 class MipEngine:
@@ -160,19 +175,32 @@ class MipEngine:
             raise MipError(f"frames of shape {f.shape[1:]} do not match {self.height}x{self.width}")
         return f
 
-    def search(self, frames, refs=None, costs=True, best=False, sad_satd=False):
+    def search(self, frames, refs=None, costs=True, best=False, sad_satd=False, out=None):
         """Full MIP search of host frames ([F,H,W] or [H,W] uint16).  Returns a dict with
         'cost' [F, nCTUs*97840] int32 and optionally 'best_mode' / 'best_cost' [F, nCTUs*5380],
-        'sad' / 'satd'."""
+        'sad' / 'satd'.  `out` may supply any of these arrays (e.g. from pinned_empty, for
+        DMA-rate transfers); the others are allocated."""
         f = self._frames(frames)
         r = None if refs is None else self._frames(refs)
         n = f.shape[0]
+        given = dict(out or {})
+
+        def buf(key, want, cols, dtype):
+            if not want:
+                return None
+            a = given.get(key)
+            if a is None:
+                return np.empty((n, cols), dtype)
+            if a.dtype != np.dtype(dtype) or a.shape != (n, cols) or not a.flags.c_contiguous:
+                raise MipError(f"out[{key!r}] must be a C-contiguous {np.dtype(dtype)} array of shape {(n, cols)}")
+            return a
+
         out = {}
-        cost = np.empty((n, self.costs_per_frame), np.int32) if costs else None
-        bm = np.empty((n, self.cus_per_frame), np.uint8) if best else None
-        bc = np.empty((n, self.cus_per_frame), np.int32) if best else None
-        sad = np.empty((n, self.costs_per_frame), np.int32) if sad_satd else None
-        satd = np.empty((n, self.costs_per_frame), np.int32) if sad_satd else None
+        cost = buf("cost", costs, self.costs_per_frame, np.int32)
+        bm = buf("best_mode", best, self.cus_per_frame, np.uint8)
+        bc = buf("best_cost", best, self.cus_per_frame, np.int32)
+        sad = buf("sad", sad_satd, self.costs_per_frame, np.int32)
+        satd = buf("satd", sad_satd, self.costs_per_frame, np.int32)
         _check(library().mip_search_frames(self._h, _ptr(f), _ptr(r), n, _ptr(cost), _ptr(bm), _ptr(bc),
                                            _ptr(sad), _ptr(satd)))
         for k, v in (("cost", cost), ("best_mode", bm), ("best_cost", bc), ("sad", sad), ("satd", satd)):
@@ -219,5 +247,5 @@ def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
     return frames_out
 
 
-__all__ = ["MipEngine", "MipError", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "library",
+__all__ = ["MipEngine", "MipError", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "library", "pinned_empty",
            "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]
