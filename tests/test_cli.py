@@ -95,6 +95,29 @@ def test_unknown_and_ambiguous_options():
 # ------------------------------------------------------------ GPU: the cost log
 @pytest.mark.gpu
 @needs_cli
+def test_device_list_shards_frames(gpu_available, tmp_path):
+    """--DeviceIndex 0,0: two engines (one per list entry, here both on GPU 0) each search a
+    contiguous half of the frames; the log of frame 0 is unchanged and --AllFrames shows
+    every frame's rows in order."""
+    W, H, N = 128, 128, 3
+    frames = synth_frames(W, H, N, 0xC12, 0)
+    write_csv(tmp_path / "in.csv", frames)
+    logs = {}
+    for dev in ("0", "0,0"):
+        prefix = str(tmp_path / ("out_" + dev.replace(",", "_")))
+        r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / "in.csv"), "-l", prefix,
+                 "--DeviceIndex", dev, "--AllFrames"])
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert f"Device Index={dev}" in r.stdout
+        logs[dev] = open(prefix + ".csv", "rb").read()
+    assert logs["0"] == logs["0,0"]
+    want = b"".join(reference_log(O.search(frames[f]), W).split(b"\n", 1)[1] if f else reference_log(O.search(frames[f]), W)
+                    for f in range(N))
+    assert logs["0,0"] == want
+
+
+@pytest.mark.gpu
+@needs_cli
 @pytest.mark.parametrize("extra,filt,kidx,sad_satd", [
     ([], None, 0, False),
     (["--FilterType", "filterFrame_2d_int_quarterCtu", "--KernelIdx", "1"], "filterFrame_2d_int_quarterCtu", 1, False),

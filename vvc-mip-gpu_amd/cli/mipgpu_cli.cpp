@@ -14,7 +14,9 @@
 // practice); this CLI prints 0 there too unless --ReportSadSatd is given.
 // Extensions: --ReportSadSatd, --AllFrames (log every frame, column CTU stays per frame,
 // a Frame column is NOT added to keep the format), --BestModes file (per-CU decision),
-// --BatchFrames N, --Threads N (log formatting threads).
+// --BatchFrames N, --Threads N (log formatting threads), and --DeviceIndex accepting a
+// list ("0,1,2,3"): the frames are sharded over those GPUs, one engine and one host thread
+// per device (frames are independent; no inter-GPU communication).
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
@@ -37,7 +39,9 @@ const char *kFilters[] = {"filterFrame_1d_int", "filterFrame_1d_float", "filterF
                           "filterFrame_2d_int_5x5_quarterCtu", "filterFrame_2d_float_5x5_quarterCtu"};
 
 struct Options {
-  int device = 0, frames = -1, kernel_idx = 0, batch = 8, threads = 0;
+  int frames = -1, kernel_idx = 0, batch = 8, threads = 0;
+  std::vector<int> devices{0};
+  std::string device_arg = "0";
   bool device_set = false, prefix_set = false, kidx_set = false, help = false;
   bool sad_satd = false, all_frames = false;
   std::string resolution, input, prefix, filter, best_modes;
@@ -57,7 +61,7 @@ const OptDef kOpts[] = {{"help", 'h', false},        {"DeviceIndex", 0, true},  
 void usage() {
   std::cout << "Allowed options:\n"
                "  -h [ --help ]                     produce help message\n"
-               "  --DeviceIndex arg (=0)            Index of the GPU device\n"
+               "  --DeviceIndex arg (=0)            Index of the GPU device (or a list: frames are sharded)\n"
                "  -f [ --FramesToBeEncoded ] arg    Number of frames to be processed\n"
                "  -s [ --Resolution ] arg           Resolution of the video, in the format 1920x1080\n"
                "  -o [ --OriginalFrames ] arg       Input file for original frames samples\n"
@@ -74,7 +78,15 @@ void usage() {
 int set_opt(Options &o, const std::string &name, const std::string &val) {
   try {
     if (name == "help") o.help = true;
-    else if (name == "DeviceIndex") o.device = std::stoi(val), o.device_set = true;
+    else if (name == "DeviceIndex") {
+      o.devices.clear();
+      std::stringstream ss(val);
+      std::string item;
+      while (std::getline(ss, item, ',')) o.devices.push_back(std::stoi(item));
+      if (o.devices.empty()) throw std::invalid_argument("empty device list");
+      o.device_arg = val;
+      o.device_set = true;
+    }
     else if (name == "FramesToBeEncoded") o.frames = std::stoi(val);
     else if (name == "Resolution") o.resolution = val;
     else if (name == "OriginalFrames") o.input = val;
@@ -136,8 +148,8 @@ int parse(int argc, char **argv, Options &o) {
 int report_parameters(const Options &o, bool alt) {
   int errors = 0;
   std::cout << "-=-= INPUT PARAMETERS =-=-" << std::endl;
-  if (!o.device_set) std::cout << "  Device index not set. Using standard value of " << o.device << "." << std::endl;
-  else std::cout << "  Device Index=" << o.device << std::endl;
+  if (!o.device_set) std::cout << "  Device index not set. Using standard value of " << o.device_arg << "." << std::endl;
+  else std::cout << "  Device Index=" << o.device_arg << std::endl;
   if (!o.prefix_set) std::cout << "  OutputPreffix log file not set. The output will not be written to any file." << std::endl;
   else std::cout << "  OutputPreffix=" << o.prefix << std::endl;
   if (o.frames >= 0) std::cout << "  FramesToBeEncoded=" << o.frames << std::endl;
@@ -296,10 +308,19 @@ int main(int argc, char **argv) {
   opts.kernel_idx = o.kernel_idx;
   opts.max_batch = std::min(o.batch, std::max(1, o.frames));
   opts.want_sad_satd = o.sad_satd ? 1 : 0;
-  mip_engine *e = nullptr;
-  if (mip_engine_create(o.device, W, H, &opts, &e) != 0) {
-    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
-    return 1;
+  std::vector<mip_engine *> engines;
+  auto destroy_all = [&]() {
+    for (mip_engine *e : engines) mip_engine_destroy(e);
+    engines.clear();
+  };
+  for (int dev : o.devices) {
+    mip_engine *e = nullptr;
+    if (mip_engine_create(dev, W, H, &opts, &e) != 0) {
+      std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
+      destroy_all();
+      return 1;
+    }
+    engines.push_back(e);
   }
   const size_t cpf = (size_t)nctus * MIP_COSTS_PER_CTU_ABI, upf = (size_t)nctus * MIP_CUS_PER_CTU_ABI;
   Pinned<int32_t> cost, sad, satd, best_cost;
@@ -309,20 +330,39 @@ int main(int argc, char **argv) {
   if (!o.best_modes.empty()) ok = ok && best.alloc(upf * o.frames) && best_cost.alloc(upf * o.frames);
   if (!ok) {
     std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
-    mip_engine_destroy(e);
+    destroy_all();
     return 1;
   }
 
+  // Frames sharded over the engines: contiguous ranges, one host thread per device.
+  const int ndev = (int)engines.size();
+  const size_t fs = (size_t)W * H;
+  std::vector<int> rcs(ndev, 0);
+  std::vector<std::string> errs(ndev);
   const auto t0 = std::chrono::steady_clock::now();  // save_startTime, main.cpp:568
-  const int rc = mip_search_frames(e, frames.data(), nullptr, o.frames, cost.data(),
-                                   best.empty() ? nullptr : best.data(), best.empty() ? nullptr : best_cost.data(),
-                                   o.sad_satd ? sad.data() : nullptr, o.sad_satd ? satd.data() : nullptr);
-  const auto t1 = std::chrono::steady_clock::now();  // save_finishTime, main.cpp:1249
-  if (rc != 0) {
-    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
-    mip_engine_destroy(e);
-    return 1;
+  {
+    std::vector<std::thread> workers;
+    for (int d = 0; d < ndev; d++) {
+      const int f0 = (int)((long long)o.frames * d / ndev), f1 = (int)((long long)o.frames * (d + 1) / ndev);
+      if (f1 <= f0) continue;
+      workers.emplace_back([&, d, f0, f1] {
+        rcs[d] = mip_search_frames(engines[d], frames.data() + f0 * fs, nullptr, f1 - f0, cost.data() + f0 * cpf,
+                                   best.empty() ? nullptr : best.data() + f0 * upf,
+                                   best.empty() ? nullptr : best_cost.data() + f0 * upf,
+                                   o.sad_satd ? sad.data() + f0 * cpf : nullptr,
+                                   o.sad_satd ? satd.data() + f0 * cpf : nullptr);
+        if (rcs[d] != 0) errs[d] = mip_last_error();
+      });
+    }
+    for (auto &w : workers) w.join();
   }
+  const auto t1 = std::chrono::steady_clock::now();  // save_finishTime, main.cpp:1249
+  for (int d = 0; d < ndev; d++)
+    if (rcs[d] != 0) {
+      std::cout << "  [!] ERROR: device " << o.devices[d] << ": " << errs[d] << std::endl;
+      destroy_all();
+      return 1;
+    }
   for (int f = 0; f < o.frames; f++) std::cout << "Current frame " << f << std::endl;
 
   std::vector<ShapeInfo> shapes(47);
@@ -338,7 +378,7 @@ int main(int argc, char **argv) {
   // reportDistortionToFile=1 in the reference even when -l is not given (writes ".csv").
   {
     FILE *fp = fopen((o.prefix + ".csv").c_str(), "w");
-    if (!fp) { perror("cannot open cost log"); mip_engine_destroy(e); return 1; }
+    if (!fp) { perror("cannot open cost log"); destroy_all(); return 1; }
     fprintf(fp, "CTU,cuSizeName,W,H,CU,X,Y,Mode,SAD,SATD,minSadHad\n");
     const int nlog = o.all_frames ? o.frames : std::min(1, o.frames);
     for (int f = 0; f < nlog; f++)
@@ -348,7 +388,7 @@ int main(int argc, char **argv) {
   }
   if (!o.best_modes.empty()) {
     FILE *fp = fopen(o.best_modes.c_str(), "w");
-    if (!fp) { perror("cannot open best-mode file"); mip_engine_destroy(e); return 1; }
+    if (!fp) { perror("cannot open best-mode file"); destroy_all(); return 1; }
     fprintf(fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,Transposed,Cost\n");
     const int ctu_cols = (W + 127) / 128;
     for (int f = 0; f < o.frames; f++)
@@ -368,6 +408,6 @@ int main(int argc, char **argv) {
   printf("TIMING RESULTS (miliseconds)\n");
   printf("Elapsed time (ms) from writing samples to reading distortion (%dx), %ld\n", o.frames, ms);
   printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n\n");
-  mip_engine_destroy(e);
+  destroy_all();
   return 0;
 }

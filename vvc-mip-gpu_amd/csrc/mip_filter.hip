@@ -292,16 +292,18 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
 
   const int c0 = 4 * (threadIdx.x & 31), r0 = 8 * (threadIdx.x >> 5);
   const short *rowp = tile + r0 * kTWP + kCO - 2 + c0;
+  // Horizontal sums are produced one row ahead of the vertical pass that consumes them
+  // (a sliding window of KS rows stays live, not all NR: fewer VGPRs, higher occupancy).
   u2 h01[NR], h23[NR];
 #pragma unroll
-  for (int r = 0; r < NR; r++) hpass<RAD, false>(rowp + r * kTWP, tt, h01[r], h23[r]);
+  for (int r = 0; r < KS - 1; r++) hpass<RAD, false>(rowp + r * kTWP, tt, h01[r], h23[r]);
 
   // Uniform scale: every window fully valid (2-D) / no frame-border class (separable).
   const bool uniform = SEP ? (qx >= 2 && qx + 128 <= W - 2 && qy >= 2 && qy + 32 <= H - 2) : !irregular;
   u2 n01[NR], n23[NR];
   if (!SEP && !uniform) {
 #pragma unroll
-    for (int r = 0; r < NR; r++) hpass<RAD, true>(rowp + r * kTWP, tt, n01[r], n23[r]);
+    for (int r = 0; r < KS - 1; r++) hpass<RAD, true>(rowp + r * kTWP, tt, n01[r], n23[r]);
   }
   const bool narrow = tsum * tsum * 1023 < 65536;  // separable part of the sum fits 16 bits
   const float rf = ref_recip((float)full);
@@ -311,6 +313,7 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int y = qy + r0 + r;
+    hpass<RAD, false>(rowp + (r + KS - 1) * kTWP, tt, h01[r + KS - 1], h23[r + KS - 1]);
     uint32_t num[4];
     if (narrow) {  // sums < 2^16: packed vertical pass
       u2 v01 = tt[0] * h01[r], v23 = tt[0] * h23[r];
@@ -345,6 +348,7 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
     } else {
       uint32_t def[4] = {0, 0, 0, 0};
       if (!SEP) {
+        hpass<RAD, true>(rowp + (r + KS - 1) * kTWP, tt, n01[r + KS - 1], n23[r + KS - 1]);
         vpass<KS>(n01 + r, t, def[0], def[1]);
         vpass<KS>(n23 + r, t, def[2], def[3]);
       }
