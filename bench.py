@@ -191,6 +191,10 @@ def main():
     ap.add_argument("--no-reference-gpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency launches")
     ap.add_argument("--no-filter", action="store_true", help="skip the filter / alternative-refs measurement")
+    ap.add_argument("--refs-filter", default=None,
+                    help="alternative references: run this reference filter (e.g. filterFrame_2d_int_quarterCtu) "
+                         "inside every step (BASELINE configs[2]/[4]); default: original references")
+    ap.add_argument("--kernel-idx", type=int, default=0, help="KernelIdx of --refs-filter")
     args = ap.parse_args()
 
     import numpy as np
@@ -210,7 +214,8 @@ def main():
 
     host = synth_frames(W, H, B, shard_seed(args.seed, rank), 0)
     frames = torch.from_numpy(host.astype(np.int16)).to(dev)
-    eng = MipEngine(W, H, device=local_rank, max_batch=B, slices_per_ctu=args.slices)
+    eng = MipEngine(W, H, device=local_rank, max_batch=B, slices_per_ctu=args.slices, filter=args.refs_filter,
+                    kernel_idx=args.kernel_idx)
     costs = torch.empty((B, eng.costs_per_frame), dtype=torch.int32, device=dev)
     stream = torch.cuda.Stream(dev)  # the search kernels and the timing events share it
 
@@ -237,6 +242,8 @@ def main():
     max_kernel_ms = dist_max(kernel_ms, world, dev)
     value, ms_per_step = aggregate(B, args.steps, world, max_elapsed)
 
+    refs_desc = ("original references (BASELINE configs[1])" if args.refs_filter is None else
+                 "alternative references %s KernelIdx %d filtered inside the step" % (args.refs_filter, args.kernel_idx))
     if rank == 0:
         alg_bytes = algorithmic_bytes_per_frame(W, H) * B
         achieved = alg_bytes / (max_kernel_ms * 1e-3) / 1e9
@@ -247,12 +254,13 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16x2/int32",
             "data": "synthetic (seeded integer generator, mipgpu/synth.py)",
-            "config": {"workload": "%dx%d frames, original references (BASELINE configs[1]); %d frames per step "
-                                   "per GPU resident in HBM; full int32 cost table written" % (W, H, B),
+            "config": {"workload": "%dx%d frames, %s; %d frames per step per GPU resident in HBM; full int32 "
+                                   "cost table written" % (W, H, refs_desc, B),
                        "width": W, "height": H, "frames_per_step": B, "parallelism": "frames sharded over %d GPU(s)" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc.get("hbm_bytes_per_launch"),
-                         "kernel": "mip_search_kernel", "kernel_ms_per_launch": round(max_kernel_ms, 4),
+                         "kernel": "mip_search_kernel" if args.refs_filter is None else "filter_kernel + mip_search_kernel",
+                         "kernel_ms_per_launch": round(max_kernel_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
             # The bound that applies: VALU issue (see the module docstring).
             "valu": valu_section(pmc, max_kernel_ms, ops),

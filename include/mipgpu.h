@@ -54,7 +54,8 @@ typedef struct {
   int kernel_idx;      /* --KernelIdx: tap set index (0..4 for 3x3, 0..2 for 5x5) */
   int max_batch;       /* frames per device batch (device buffers sized for this); >= 1 */
   int want_sad_satd;   /* also produce the SAD / SATD tables (MAX_PERFORMANCE_DIST=0) */
-  int slices_per_ctu;  /* workgroups per 64x64 CTU quadrant in the search kernel; 0 = auto */
+  int slices_per_ctu;  /* workgroups per 64x64 CTU quadrant in the search kernel; 0 = auto
+                          (chosen per launch: more, smaller workgroups for small batches) */
 } mip_opts;
 
 typedef struct mip_engine mip_engine;

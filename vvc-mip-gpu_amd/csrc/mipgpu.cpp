@@ -218,12 +218,31 @@ struct mip_engine {
   uint16_t *d_frames = nullptr, *d_refs = nullptr;
   int32_t *d_costs = nullptr, *d_sad = nullptr, *d_satd = nullptr, *d_best_cost = nullptr;
   uint8_t *d_best = nullptr;
-  mipgpu::WaveTask *d_tasks = nullptr;
-  mipgpu::Job *d_jobs = nullptr;
-  int *d_lists = nullptr;
+  // Work lists, one set per slice count (workgroups per CTU quadrant): small batches need
+  // more, smaller workgroups to fill the chip (see pick_work).
+  struct Work {
+    int slices = 1;
+    mipgpu::WaveTask *d_tasks = nullptr;
+    mipgpu::Job *d_jobs = nullptr;
+    int *d_lists = nullptr;
+  };
+  std::vector<Work> work;
   uint8_t *d_tables = nullptr;
-  int slices = 1;
 };
+
+namespace {
+// Slice count for a launch of `nframes`: ~4 quadrant workgroups per CU slot or more
+// (measured on MI355X at 1080p: 1 frame -> 4 slices 4246 vs 3444 frames/s, 2-4 frames -> 2,
+// >= 8 frames -> 1).
+const mip_engine::Work &pick_work(const mip_engine *e, int nframes) {
+  const long long wg1 = 4LL * e->nctus * nframes;  // workgroups at one slice
+  const int want = wg1 < 1000 ? 4 : (wg1 < 4500 ? 2 : 1);
+  const mip_engine::Work *best = &e->work[0];
+  for (const mip_engine::Work &w : e->work)
+    if (std::abs(w.slices - want) < std::abs(best->slices - want)) best = &w;
+  return *best;
+}
+}  // namespace
 
 extern "C" {
 
@@ -273,9 +292,11 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
-                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tasks,
-                  (void *)e->d_jobs, (void *)e->d_lists, (void *)e->d_tables})
+                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables})
     if (p) (void)hipFree(p);
+  for (const mip_engine::Work &w : e->work)
+    for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists})
+      if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
   delete e;
@@ -326,19 +347,28 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   }
   ALLOC(e->d_best, ncu);
   ALLOC(e->d_best_cost, ncu * 4);
-  e->slices = o.slices_per_ctu > 0 ? o.slices_per_ctu : 1;
-  const WorkLists wl = build_work(e->slices, mipgpu::search_waves_per_group());
-  ALLOC(e->d_tasks, std::max<size_t>(1, wl.tasks.size()) * sizeof(mipgpu::WaveTask));
-  ALLOC(e->d_jobs, std::max<size_t>(1, wl.jobs.size()) * sizeof(mipgpu::Job));
-  ALLOC(e->d_lists, wl.list_begin.size() * sizeof(int));
+  std::vector<int> slice_set;
+  if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
+  else slice_set = {1, 2, 4};
+  for (int sl : slice_set) {
+    const WorkLists wl = build_work(sl, mipgpu::search_waves_per_group());
+    mip_engine::Work w;
+    w.slices = sl;
+    e->work.push_back(w);
+    mip_engine::Work &ew = e->work.back();
+    ALLOC(ew.d_tasks, std::max<size_t>(1, wl.tasks.size()) * sizeof(mipgpu::WaveTask));
+    ALLOC(ew.d_jobs, std::max<size_t>(1, wl.jobs.size()) * sizeof(mipgpu::Job));
+    ALLOC(ew.d_lists, wl.list_begin.size() * sizeof(int));
+    if ((!wl.tasks.empty() &&
+         (hipMemcpy(ew.d_tasks, wl.tasks.data(), wl.tasks.size() * sizeof(mipgpu::WaveTask), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(ew.d_jobs, wl.jobs.data(), wl.jobs.size() * sizeof(mipgpu::Job), hipMemcpyHostToDevice) != hipSuccess)) ||
+        hipMemcpy(ew.d_lists, wl.list_begin.data(), wl.list_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail("uploading work lists failed"));
+  }
   const std::vector<uint8_t> tab = build_tables();
   ALLOC(e->d_tables, tab.size());
 #undef ALLOC
-  if ((!wl.tasks.empty() &&
-       (hipMemcpy(e->d_tasks, wl.tasks.data(), wl.tasks.size() * sizeof(mipgpu::WaveTask), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(e->d_jobs, wl.jobs.data(), wl.jobs.size() * sizeof(mipgpu::Job), hipMemcpyHostToDevice) != hipSuccess)) ||
-      hipMemcpy(e->d_lists, wl.list_begin.data(), wl.list_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(e->d_tables, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpy(e->d_tables, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail("uploading static tables failed"));
   *out = e;
   return 0;
@@ -372,31 +402,32 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.cost = d_costs;
   a.sad = d_sad;
   a.satd = d_satd;
-  a.tasks = e->d_tasks;
-  a.jobs = e->d_jobs;
-  a.list_begin = e->d_lists;
+  const mip_engine::Work &work = pick_work(e, nframes);
+  a.tasks = work.d_tasks;
+  a.jobs = work.d_jobs;
+  a.list_begin = work.d_lists;
   a.tables = reinterpret_cast<const uint4 *>(e->d_tables);
   a.width = e->width;
   a.height = e->height;
   a.ctu_cols = e->ctu_cols;
   a.nctus = e->nctus;
-  a.slices = e->slices;
+  a.slices = work.slices;
   // MIPGPU_WAVE_TIMING=file (profiling): per-task cycles appended to `file` (synchronous;
   // one binary record of uint64 [workgroup][wave][kClockSlots] per launch), and the task
   // lists to `file`.tasks once.
   static const char *timing = getenv("MIPGPU_WAVE_TIMING");
   std::vector<uint64_t> clocks;
   if (timing) {
-    const size_t n = (size_t)4 * e->slices * e->nctus * nframes * mipgpu::kClockSlots;
+    const size_t n = (size_t)4 * work.slices * e->nctus * nframes * mipgpu::kClockSlots;
     HIP_TRY(hipMalloc((void **)&a.wave_clock, n * 8));
     HIP_TRY(hipMemsetAsync(a.wave_clock, 0, n * 8, s));
     clocks.resize(n);
     static bool dumped = false;
     if (!dumped) {
       dumped = true;
-      const WorkLists wl = build_work(e->slices, mipgpu::search_waves_per_group());
+      const WorkLists wl = build_work(work.slices, mipgpu::search_waves_per_group());
       if (FILE *f = fopen((std::string(timing) + ".tasks").c_str(), "w")) {
-        fprintf(f, "{\"slices\": %d, \"list_begin\": [", e->slices);
+        fprintf(f, "{\"slices\": %d, \"list_begin\": [", work.slices);
         for (size_t i = 0; i < wl.list_begin.size(); i++) fprintf(f, "%s%d", i ? ", " : "", wl.list_begin[i]);
         fprintf(f, "], \"tasks\": [");
         for (size_t i = 0; i < wl.tasks.size(); i++)
