@@ -191,6 +191,8 @@ def main():
     ap.add_argument("--no-reference-gpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-frame latency launches")
     ap.add_argument("--no-filter", action="store_true", help="skip the filter / alternative-refs measurement")
+    ap.add_argument("--no-end-to-end", action="store_true",
+                    help="skip the host-buffer measurement (its launches are half batches; keep them out of profiles)")
     ap.add_argument("--refs-filter", default=None,
                     help="alternative references: run this reference filter (e.g. filterFrame_2d_int_quarterCtu) "
                          "inside every step (BASELINE configs[2]/[4]); default: original references")
@@ -282,6 +284,7 @@ def main():
         if world == 1:
             if not args.no_cpu_baseline:
                 res["cpu_baseline"] = cpu_baseline(W, H, args.seed)
+        if world == 1 and not args.no_end_to_end:
             # Host-buffer path incl. PCIe (informative, never `value`): page-locked buffers
             # (mip_host_alloc; transfers overlap the next chunk's search) and pageable ones.
             from mipgpu import pinned_empty
@@ -300,12 +303,12 @@ def main():
                                  "note": "host frames in, host int32 cost tables out (H2D + search + D2H, "
                                          "%.1f MB per frame over PCIe); value: page-locked buffers" %
                                          (algorithmic_bytes_per_frame(W, H) / 1e6)}
-            if not args.no_reference_gpu:
-                ref = reference_gpu(W, H, min(B, 4), args.seed)
-                if ref is not None:
-                    res["reference_gpu"] = ref
-                    if ref.get("value"):
-                        res["speedup_vs_reference_gpu"] = round(value / ref["value"], 2)
+        if world == 1 and not args.no_reference_gpu:
+            ref = reference_gpu(W, H, min(B, 4), args.seed)
+            if ref is not None:
+                res["reference_gpu"] = ref
+                if ref.get("value"):
+                    res["speedup_vs_reference_gpu"] = round(value / ref["value"], 2)
         print(json.dumps(res), flush=True)
     eng.close()
     if world > 1:

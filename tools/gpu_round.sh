@@ -24,7 +24,7 @@ cat "$OUT/bench.json"
 step rocprof
 rm -rf "$OUT/prof"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-  python bench.py --no-cpu-baseline --no-reference-gpu --no-latency --steps 10 > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
+  python bench.py --no-cpu-baseline --no-reference-gpu --no-latency --no-end-to-end --steps 10 > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
   || { tail -20 "$OUT/prof.err"; exit 1; }
 find "$OUT/prof" -name "*stats*" | head
 step done

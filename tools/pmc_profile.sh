@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out}/pmc
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:-"--frames-per-step 32 --steps 3 --warmup 1 --no-cpu-baseline --no-reference-gpu --no-latency"}
+ARGS=${BENCH_ARGS:-"--frames-per-step 32 --steps 3 --warmup 1 --no-cpu-baseline --no-reference-gpu --no-latency --no-end-to-end"}
 i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
