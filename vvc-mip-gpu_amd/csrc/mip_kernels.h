@@ -36,8 +36,8 @@ constexpr int class_size_id(int w, int h) { return (w == 4 && h == 4) ? 0 : ((w 
 // Row parts: classes with few CUs per quadrant split each CU's rows over V lanes per strip
 // so that a task still fills the wave.
 constexpr int class_row_parts(int w, int h) {
-  return (w == 64 || (w == 16 && h >= 16)) ? 4
-         : ((w == 32 && h >= 16) || (w == 4 && h >= 16)) ? 2 : 1;
+  return (w == 64 || (w == 16 && h >= 32)) ? 4
+         : ((w == 32 && h >= 16) || (w == 4 && h >= 16) || (w == 16 && h == 16)) ? 2 : 1;
 }
 constexpr int class_slots(int w, int h) { return 64 / ((w / 4) * class_row_parts(w, h)); }
 
