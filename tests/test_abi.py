@@ -3,6 +3,7 @@ Only host-side geometry helpers are called (no GPU needed)."""
 import ctypes
 import os
 import re
+import sys
 import subprocess
 
 import pytest
@@ -63,3 +64,14 @@ def test_filter_names_follow_reference_whitelist():
     assert mipgpu.filter_index(None) == mipgpu.FILTER_NONE
     with pytest.raises(mipgpu.MipError):
         mipgpu.filter_index("filterFrame_2d")  # half-CTU kernel, not whitelisted (constants.h:25-34)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """The product path has no CPU fallback: without libmipgpu.so the binding raises."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import mipgpu\n"
+            "try:\n    mipgpu.MipEngine(128, 128)\nexcept mipgpu.MipError as e:\n    print('MipError', e)\n"
+            % os.path.join(REPO, "vvc-mip-gpu_amd"))
+    env = dict(os.environ, MIPGPU_LIB=str(tmp_path / "absent.so"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert "MipError" in out.stdout and "no CPU fallback" in out.stdout, out.stdout + out.stderr

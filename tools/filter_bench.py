@@ -30,4 +30,19 @@ for name in FILTERS:
     ms = e0.elapsed_time(e1) / REPS
     gbs = 4 * W * H * B / (ms * 1e-3) / 1e9
     res[name] = {"ms_per_launch": round(ms, 4), "GB/s": round(gbs, 1), "frac_of_8TB/s": round(gbs / 8000, 3)}
-print(json.dumps({"workload": "%dx%d x %d frames, kernel_idx 0" % (W, H, B), "filters": res}, indent=1))
+# Calibration: a plain device-to-device copy of the same bytes (torch, same stream) -- the
+# practically reachable read+write bandwidth for this size.
+for _ in range(3):
+    with torch.cuda.stream(s):
+        out.copy_(frames)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(s)
+with torch.cuda.stream(s):
+    for _ in range(REPS):
+        out.copy_(frames)
+e1.record(s)
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / REPS
+copy = {"ms_per_launch": round(ms, 4), "GB/s": round(4 * W * H * B / (ms * 1e-3) / 1e9, 1)}
+print(json.dumps({"workload": "%dx%d x %d frames, kernel_idx 0" % (W, H, B), "filters": res,
+                  "copy_calibration": copy}, indent=1))
