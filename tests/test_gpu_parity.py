@@ -117,6 +117,26 @@ def test_batched_device_api_matches_host_api(gpu_available):
         assert np.array_equal(host["cost"][f], O.search(frames[f], refs))
 
 
+def test_many_launches_on_two_streams(gpu_available):
+    """The persistent search kernel takes its items from one of 16 device counters per
+    engine; 40 back-to-back launches alternating between two streams (and frame counts, so
+    the grids differ) must reuse the counters safely and all give the same tables."""
+    import torch
+    w, h = 264, 200  # edge CTUs in both directions
+    frames = synth_frames(w, h, 3, 0x51, 0)
+    want = np.stack([O.search(frames[f]) for f in range(3)])
+    d = torch.from_numpy(frames.astype(np.int16)).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    with MipEngine(w, h, max_batch=3) as eng:
+        outs = []
+        for i in range(40):
+            n = 1 + i % 3
+            outs.append((n, eng.search_device(d[:n], stream=streams[i % 2])))
+        torch.cuda.synchronize()
+        for n, c in outs:
+            assert np.array_equal(c.cpu().numpy(), want[:n])
+
+
 def test_errors_are_loud(gpu_available):
     with pytest.raises(MipError):
         MipEngine(130, 64)  # width not a multiple of 4

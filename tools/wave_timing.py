@@ -33,8 +33,10 @@ eng.search_device(frames, costs=costs)
 torch.cuda.synchronize()
 tl = json.load(open(path + ".tasks"))
 slices, lb, tasks = tl["slices"], tl["list_begin"], tl["tasks"]
+# items are (frame, CTU, quadrant, slice); complete CTUs only (variant-0 lists)
 clk = np.fromfile(path, dtype=np.uint64).astype(np.int64).reshape(B, eng.nctus, 4, slices, SLOTS)
-mean_clk = clk.mean(axis=(0, 1))                       # [quad, slice, task]
+full = [c for c in range(eng.nctus) if 128 * (c % (W // 128 + (W % 128 > 0)) + 1) <= W and 128 * (c // (W // 128 + (W % 128 > 0)) + 1) <= H]
+mean_clk = clk[:, full].mean(axis=(0, 1))               # [quad, slice, task]
 rows = {}
 for q in range(4):
     for sl in range(slices):

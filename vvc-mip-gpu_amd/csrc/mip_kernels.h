@@ -49,15 +49,24 @@ struct SearchArgs {
   int32_t *satd;          // optional, same layout
   const WaveTask *tasks;  // per (quadrant, wave) task lists, concatenated
   const Job *jobs;
-  const int *list_begin;  // task list of (quadrant q, slice s): [list_begin[q*slices+s], list_begin[q*slices+s+1])
+  const int *list_begin;  // task list of (CTU variant v, quadrant q, slice s), index l = (4v+q)*slices+s:
+                          // [list_begin[l], list_begin[l+1])
+  const uint32_t *fill;   // unavailable cost entries of (v, q) (uint4 units inside the CTU's cost
+  const int *fill_begin;  // block): [fill_begin[4v+q], fill_begin[4v+q+1])
   const uint4 *tables;    // kTableBytes: MIP matrices for the MFMA, see below
   int width, height;
   int ctu_cols, nctus;
   int slices;             // workgroups (task lists) per CTU quadrant
+  uint32_t *queue;        // item counter pair {next item, workgroups done}, zero at launch;
+                          // the kernel leaves it zero again
+  uint32_t nitems;        // frames * nctus * 4 * slices (set by launch_search)
   uint64_t *wave_clock;   // profiling (MIPGPU_WAVE_TIMING): [workgroup][kClockSlots] cycles per
                           // task of the workgroup's list; else null
 };
 constexpr int kClockSlots = 128;
+// CTU variants: bit 0 = the frame ends inside the CTU horizontally, bit 1 = vertically
+// (mipgpu.cpp build_work); their lists omit the CUs that are not completely inside the frame.
+constexpr int kCtuVariants = 4;
 
 // MIP matrices, restated for an exact f16 MFMA (mip_search.hip, phase A).  The reference
 // computes pred_j = clamp(((32 - 32*sum_k p_k + sum_k p_k*w_jk) >> 6) + b0, 0, 1023) with

@@ -26,6 +26,9 @@
 // Bit-exactness: every step restates the reference integer semantics (citations inline);
 // tests/test_gpu_parity.py checks the tables bit for bit against the C oracle, which is
 // pinned to the reference kernels' own outputs (tests/golden/).
+#include <algorithm>
+#include <cstdlib>
+
 #include "mip_kernels.h"
 #include "mip_tables.h"
 
@@ -563,7 +566,6 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   }
   OrigRows<H> orig;
   orig.load(x.org, c.lx + x0, c.ly);
-  const bool avail = x.fx0 + c.lx + W <= a.width && x.fy0 + c.ly + H <= a.height;
   const size_t cbase = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
   const uint32_t *mine = reinterpret_cast<const uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
   const Red<G::R> red{mine, 0};
@@ -610,13 +612,11 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
     acc.satd1 = group_sum<GS>(acc.satd1);
     if (active && sub == GS - 1) {
       const size_t idx = cbase + 2 * q;
-      const int c0 = avail ? min(2 * (int)acc.sad0, (int)acc.satd0) : kUnavailable;  // intra.cl:1166
-      const int c1 = avail ? min(2 * (int)acc.sad1, (int)acc.satd1) : kUnavailable;
+      // every CU of a task lies inside the frame (build_work); intra.cl:1166
+      const int c0 = min(2 * (int)acc.sad0, (int)acc.satd0), c1 = min(2 * (int)acc.sad1, (int)acc.satd1);
       *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
-      if (a.sad)
-        *reinterpret_cast<int2 *>(a.sad + idx) = avail ? make_int2(acc.sad0, acc.sad1) : make_int2(kUnavailable, kUnavailable);
-      if (a.satd)
-        *reinterpret_cast<int2 *>(a.satd + idx) = avail ? make_int2(acc.satd0, acc.satd1) : make_int2(kUnavailable, kUnavailable);
+      if (a.sad) *reinterpret_cast<int2 *>(a.sad + idx) = make_int2(acc.sad0, acc.sad1);
+      if (a.satd) *reinterpret_cast<int2 *>(a.satd + idx) = make_int2(acc.satd0, acc.satd1);
     }
   }
 }
@@ -666,54 +666,92 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   uint8_t *zero = w + kTableBytes;
   uint8_t *waves = zero + kZeroBytes;
 
-  const int slice = blockIdx.x % a.slices, quad = blockIdx.x / a.slices;
-  const int ctu = blockIdx.y, frame = blockIdx.z;
-  const int ctu_x = 128 * (ctu % a.ctu_cols), ctu_y = 128 * (ctu / a.ctu_cols);
-  const int fx0 = ctu_x + 64 * (quad & 1), fy0 = ctu_y + 64 * (quad >> 1);
-  const size_t fofs = (size_t)frame * a.width * a.height;
-
-  stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0);
-  if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0);
   for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(w)[i] = a.tables[i];
   for (int i = threadIdx.x; i < kZeroBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
   uint32_t *next_task = reinterpret_cast<uint32_t *>(waves + kWaves * kWaveBytes);
-  if (threadIdx.x == 0) *next_task = 0;
-  __syncthreads();
-
+  uint32_t *cur_item = next_task + 1;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const Ctx x{&a, org, ref, w, zero, waves + wave * kWaveBytes, ctu, frame, fx0, fy0};
-  const RefTile<ALT> rt{ref};
-  // Waves take the workgroup's tasks (longest first) from an LDS counter, so early
-  // finishers pick up the slack of waves the SIMD arbiter serves later.
-  const int list = quad * a.slices + slice;
-  const int tbase = a.list_begin[list], ntasks = a.list_begin[list + 1] - tbase;
-  uint64_t *clk = a.wave_clock ? a.wave_clock + (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) *
-                                      kClockSlots : nullptr;
+  const int per_ctu = 4 * a.slices;
+
+  // Persistent workgroups (as many as are resident) take items = (frame, CTU, quadrant,
+  // slice) from a device-wide counter, in order: the hardware's static round-robin of
+  // workgroups over XCDs and CUs cannot balance items of unequal cost (edge CTUs).
   for (;;) {
-    uint32_t tn = 0;
-    if (lane == 0) tn = atomicAdd(next_task, 1u);
-    const int t = (int)__builtin_amdgcn_readfirstlane(tn);
-    if (t >= ntasks) break;
-    const uint64_t c0 = clk ? __builtin_readcyclecounter() : 0;
-    const WaveTask task = a.tasks[tbase + t];
-    switch (task.cls) {
+    if (threadIdx.x == 0) {
+      *cur_item = atomicAdd(a.queue, 1u);
+      *next_task = 0;
+    }
+    __syncthreads();
+    const uint32_t item = *cur_item;
+    if (item >= a.nitems) break;  // workgroup-uniform
+    const int gx = item % per_ctu, ctu = (item / per_ctu) % a.nctus, frame = item / (per_ctu * a.nctus);
+    const int slice = gx % a.slices, quad = gx / a.slices;
+    const int ctu_x = 128 * (ctu % a.ctu_cols), ctu_y = 128 * (ctu / a.ctu_cols);
+    const int fx0 = ctu_x + 64 * (quad & 1), fy0 = ctu_y + 64 * (quad >> 1);
+    const size_t fofs = (size_t)frame * a.width * a.height;
+    const int var = (ctu_x + 128 > a.width ? 1 : 0) | (ctu_y + 128 > a.height ? 2 : 0);
+    const int vq = var * 4 + quad, list = vq * a.slices + slice;
+    const int tbase = a.list_begin[list], ntasks = a.list_begin[list + 1] - tbase;
+
+    // CUs not completely inside the frame (edge CTUs): MIP_COST_UNAVAILABLE, no search
+    if (var) {
+      const size_t cbase = ((size_t)frame * a.nctus + ctu) * (MIP_COSTS_PER_CTU / 4);
+      const int f0 = a.fill_begin[vq], nf = a.fill_begin[vq + 1] - f0;
+      const uint4 un = make_uint4(kUnavailable, kUnavailable, kUnavailable, kUnavailable);
+      for (int i = slice * blockDim.x + threadIdx.x; i < nf; i += a.slices * blockDim.x) {
+        const size_t o = cbase + a.fill[f0 + i];
+        reinterpret_cast<uint4 *>(a.cost)[o] = un;
+        if (a.sad) reinterpret_cast<uint4 *>(a.sad)[o] = un;
+        if (a.satd) reinterpret_cast<uint4 *>(a.satd)[o] = un;
+      }
+    }
+    if (ntasks > 0) {  // workgroup-uniform
+      stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0);
+      if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0);
+      __syncthreads();
+
+      const Ctx x{&a, org, ref, w, zero, waves + wave * kWaveBytes, ctu, frame, fx0, fy0};
+      const RefTile<ALT> rt{ref};
+      // Waves take the item's tasks (longest first) from an LDS counter, so early
+      // finishers pick up the slack of waves the SIMD arbiter serves later.
+      uint64_t *clk = a.wave_clock ? a.wave_clock + (size_t)item * kClockSlots : nullptr;
+      for (;;) {
+        uint32_t tn = 0;
+        if (lane == 0) tn = atomicAdd(next_task, 1u);
+        const int t = (int)__builtin_amdgcn_readfirstlane(tn);
+        if (t >= ntasks) break;
+        const uint64_t c0 = clk ? __builtin_readcyclecounter() : 0;
+        const WaveTask task = a.tasks[tbase + t];
+        switch (task.cls) {
 #define MIP_CASE(idx, W, H)                                 \
   case idx:                                                 \
     static_assert(size_class(W, H) == idx, "class table");  \
     if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)        \
       run_task<W, H, ALT>(x, rt, task, lane);               \
     break;
-      MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
-      MIP_CASE(4, 32, 8) MIP_CASE(5, 8, 32) MIP_CASE(6, 16, 16) MIP_CASE(7, 16, 8)
-      MIP_CASE(8, 8, 16) MIP_CASE(9, 32, 4) MIP_CASE(10, 4, 32) MIP_CASE(11, 16, 4)
-      MIP_CASE(12, 4, 16) MIP_CASE(13, 8, 8) MIP_CASE(14, 8, 4) MIP_CASE(15, 4, 8)
-      MIP_CASE(16, 4, 4)
+          MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
+          MIP_CASE(4, 32, 8) MIP_CASE(5, 8, 32) MIP_CASE(6, 16, 16) MIP_CASE(7, 16, 8)
+          MIP_CASE(8, 8, 16) MIP_CASE(9, 32, 4) MIP_CASE(10, 4, 32) MIP_CASE(11, 16, 4)
+          MIP_CASE(12, 4, 16) MIP_CASE(13, 8, 8) MIP_CASE(14, 8, 4) MIP_CASE(15, 4, 8)
+          MIP_CASE(16, 4, 4)
 #undef MIP_CASE
-      default: break;
+          default: break;
+        }
+        if (clk && lane == 0 && t < kClockSlots) clk[t] = __builtin_readcyclecounter() - c0;
+      }
     }
-    if (clk && lane == 0 && t < kClockSlots) clk[t] = __builtin_readcyclecounter() - c0;
+    __syncthreads();  // the tile and cur_item are rewritten for the next item
+  }
+  // The last workgroup to leave resets the counter pair for the next launch that uses it
+  // (the host never runs two launches on one pair at the same time).
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(a.queue + 1, 1u) == gridDim.x - 1) {
+      atomicExch(a.queue, 0u);
+      atomicExch(a.queue + 1, 0u);
+    }
   }
 }
 
@@ -741,14 +779,38 @@ size_t search_lds_bytes(bool alt) {
   return (size_t)(kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes + (size_t)kWaves * kWaveBytes + 16;
 }
 
-hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, hipStream_t s) {
-  if (a.slices < 1) return hipErrorInvalidValue;
-  const dim3 grid(4 * a.slices, a.nctus, nframes);
+// Workgroups resident on the device at once (persistent grid size).
+static int resident_groups(bool alt) {
+  static int cached[2] = {0, 0};
+  int &n = cached[alt ? 1 : 0];
+  if (n == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    const hipError_t e = alt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<true>, 64 * kWaves,
+                                                                            search_lds_bytes(true))
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<false>, 64 * kWaves,
+                                                                            search_lds_bytes(false));
+    if (e != hipSuccess || per_cu < 1) return 0;
+    n = cus * per_cu;
+  }
+  return n;
+}
+
+hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, hipStream_t s) {
+  if (args.slices < 1 || !args.queue) return hipErrorInvalidValue;
+  SearchArgs a = args;
+  a.nitems = (uint32_t)(4 * a.slices) * a.nctus * nframes;
+  const int resident = resident_groups(alt_refs);
+  if (resident < 1) return hipErrorInvalidDevice;
+  const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
+  const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const size_t lds = search_lds_bytes(alt_refs);
   if (alt_refs)
-    hipLaunchKernelGGL(mip_search_kernel<true>, grid, dim3(64 * kWaves), lds, s, a);
+    hipLaunchKernelGGL(mip_search_kernel<true>, dim3(groups), dim3(64 * kWaves), lds, s, a);
   else
-    hipLaunchKernelGGL(mip_search_kernel<false>, grid, dim3(64 * kWaves), lds, s, a);
+    hipLaunchKernelGGL(mip_search_kernel<false>, dim3(groups), dim3(64 * kWaves), lds, s, a);
   return hipGetLastError();
 }
 

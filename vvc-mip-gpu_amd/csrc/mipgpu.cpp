@@ -101,10 +101,17 @@ std::vector<uint8_t> build_tables() {
 // lists (one per workgroup); each list stays in decreasing cost order, and the waves of a
 // workgroup take its tasks dynamically.  Costs are VALU-instruction estimates per lane.
 // MIPGPU_SHAPE_FILTER="i,j,..." (profiling knob) restricts the search to those shapes.
+// Edge CTUs: a CTU in the last column / row of a frame whose width / height is not a
+// multiple of 128 holds CUs that are not completely inside the frame (the reference leaves
+// their costs undefined, here they are MIP_COST_UNAVAILABLE).  Such CUs get no task: each of
+// the 4 CTU variants (bit 0: partial width, bit 1: partial height) has its own lists, and a
+// fill list of the unavailable cost entries (16-byte units inside the CTU's cost block).
 struct WorkLists {
   std::vector<mipgpu::WaveTask> tasks;
   std::vector<mipgpu::Job> jobs;
-  std::vector<int> list_begin;
+  std::vector<int> list_begin;   // [variant][quadrant][slice] + 1
+  std::vector<uint32_t> fill;    // unavailable cost entries, uint4 index inside the CTU block
+  std::vector<int> fill_begin;   // [variant][quadrant] + 1
 };
 
 bool shape_selected(int s) {
@@ -136,9 +143,14 @@ double pair_cost(int cls, int ncu) {
   return blocks * 200.0 + mfma * 12.0 + 40.0;
 }
 
-WorkLists build_work(int slices, int waves) {
+WorkLists build_work(int slices, int waves, int width, int height) {
   WorkLists wl;
-  for (int q = 0; q < 4; q++) {
+  for (int vq = 0; vq < 4 * mipgpu::kCtuVariants; vq++) {
+    const int var = vq / 4, q = vq % 4;
+    // samples of the CTU inside the frame (variant 0: the whole CTU)
+    const int avw = (var & 1) && width % 128 ? width % 128 : 128;
+    const int avh = (var & 2) && height % 128 ? height % 128 : 128;
+    wl.fill_begin.push_back((int)wl.fill.size());
     struct Piece { mipgpu::WaveTask t; double cost; };
     std::vector<Piece> pieces;
     std::vector<std::vector<mipgpu::Job>> cls_cus(mipgpu::kNumClasses);
@@ -149,6 +161,11 @@ WorkLists build_work(int slices, int waves) {
       for (int cu = 0; cu < sd.ncu; cu++) {
         const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
         if (x / 64 != (q & 1) || y / 64 != (q >> 1)) continue;
+        if (x + sd.w > avw || y + sd.h > avh) {
+          const uint32_t off = sd.cost_offset + cu * 2 * sd.modes;  // multiple of 4 entries
+          for (uint32_t u = 0; u < (uint32_t)(2 * sd.modes) / 4; u++) wl.fill.push_back(off / 4 + u);
+          continue;
+        }
         cls_cus[cls].push_back(mipgpu::Job{(uint32_t)(sd.cost_offset + cu * 2 * sd.modes), (uint8_t)(x % 64),
                                            (uint8_t)(y % 64), 0});
       }
@@ -172,7 +189,7 @@ WorkLists build_work(int slices, int waves) {
       }
     }
     // cut long tasks into pair ranges
-    const double cap = total / (slices * waves) / cut_factor();
+    const double cap = std::max(1.0, total / (slices * waves) / cut_factor());
     std::vector<Piece> cut;
     for (const Piece &p : pieces) {
       const int np = p.t.q1 - p.t.q0;
@@ -200,6 +217,7 @@ WorkLists build_work(int slices, int waves) {
     }
   }
   wl.list_begin.push_back((int)wl.tasks.size());
+  wl.fill_begin.push_back((int)wl.fill.size());
   return wl;
 }
 
@@ -225,9 +243,19 @@ struct mip_engine {
     mipgpu::WaveTask *d_tasks = nullptr;
     mipgpu::Job *d_jobs = nullptr;
     int *d_lists = nullptr;
+    uint32_t *d_fill = nullptr;
+    int *d_fill_begin = nullptr;
   };
   std::vector<Work> work;
   uint8_t *d_tables = nullptr;
+  // Item-counter pairs of the persistent search kernel, used round robin; a pair is reused
+  // only after the launch that last used it has completed (stream wait on its event), so
+  // launches on different streams never share one.
+  static constexpr int kQueueSlots = 16;
+  uint32_t *d_queue = nullptr;
+  hipEvent_t queue_done[kQueueSlots] = {};
+  bool queue_used[kQueueSlots] = {};
+  unsigned queue_seq = 0;
 };
 
 namespace {
@@ -294,8 +322,11 @@ int mip_engine_destroy(mip_engine *e) {
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables})
     if (p) (void)hipFree(p);
+  if (e->d_queue) (void)hipFree(e->d_queue);
+  for (hipEvent_t ev : e->queue_done)
+    if (ev) (void)hipEventDestroy(ev);
   for (const mip_engine::Work &w : e->work)
-    for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists})
+    for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin})
       if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -346,12 +377,17 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     ALLOC(e->d_satd, ncost * 4);
   }
   ALLOC(e->d_best, ncu);
+  ALLOC(e->d_queue, 2 * mip_engine::kQueueSlots * sizeof(uint32_t));
+  if (hipMemset(e->d_queue, 0, 2 * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
+    return cleanup(fail("hipMemset failed"));
+  for (hipEvent_t &ev : e->queue_done)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   ALLOC(e->d_best_cost, ncu * 4);
   std::vector<int> slice_set;
   if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
   else slice_set = {1, 2, 4};
   for (int sl : slice_set) {
-    const WorkLists wl = build_work(sl, mipgpu::search_waves_per_group());
+    const WorkLists wl = build_work(sl, mipgpu::search_waves_per_group(), width, height);
     mip_engine::Work w;
     w.slices = sl;
     e->work.push_back(w);
@@ -359,6 +395,12 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     ALLOC(ew.d_tasks, std::max<size_t>(1, wl.tasks.size()) * sizeof(mipgpu::WaveTask));
     ALLOC(ew.d_jobs, std::max<size_t>(1, wl.jobs.size()) * sizeof(mipgpu::Job));
     ALLOC(ew.d_lists, wl.list_begin.size() * sizeof(int));
+    ALLOC(ew.d_fill, std::max<size_t>(1, wl.fill.size()) * sizeof(uint32_t));
+    ALLOC(ew.d_fill_begin, wl.fill_begin.size() * sizeof(int));
+    if ((!wl.fill.empty() &&
+         hipMemcpy(ew.d_fill, wl.fill.data(), wl.fill.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(ew.d_fill_begin, wl.fill_begin.data(), wl.fill_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail("uploading fill lists failed"));
     if ((!wl.tasks.empty() &&
          (hipMemcpy(ew.d_tasks, wl.tasks.data(), wl.tasks.size() * sizeof(mipgpu::WaveTask), hipMemcpyHostToDevice) != hipSuccess ||
           hipMemcpy(ew.d_jobs, wl.jobs.data(), wl.jobs.size() * sizeof(mipgpu::Job), hipMemcpyHostToDevice) != hipSuccess)) ||
@@ -406,6 +448,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.tasks = work.d_tasks;
   a.jobs = work.d_jobs;
   a.list_begin = work.d_lists;
+  a.fill = work.d_fill;
+  a.fill_begin = work.d_fill_begin;
   a.tables = reinterpret_cast<const uint4 *>(e->d_tables);
   a.width = e->width;
   a.height = e->height;
@@ -425,7 +469,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     static bool dumped = false;
     if (!dumped) {
       dumped = true;
-      const WorkLists wl = build_work(work.slices, mipgpu::search_waves_per_group());
+      const WorkLists wl = build_work(work.slices, mipgpu::search_waves_per_group(), e->width, e->height);
       if (FILE *f = fopen((std::string(timing) + ".tasks").c_str(), "w")) {
         fprintf(f, "{\"slices\": %d, \"list_begin\": [", work.slices);
         for (size_t i = 0; i < wl.list_begin.size(); i++) fprintf(f, "%s%d", i ? ", " : "", wl.list_begin[i]);
@@ -437,7 +481,12 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
       }
     }
   }
+  const int slot = (int)(e->queue_seq++ % mip_engine::kQueueSlots);
+  if (e->queue_used[slot]) HIP_TRY(hipStreamWaitEvent(s, e->queue_done[slot], 0));
+  a.queue = e->d_queue + 2 * slot;
   HIP_TRY(mipgpu::launch_search(a, nframes, alt, s));
+  HIP_TRY(hipEventRecord(e->queue_done[slot], s));
+  e->queue_used[slot] = true;
   if (timing) {
     HIP_TRY(hipMemcpyAsync(clocks.data(), a.wave_clock, clocks.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
