@@ -95,8 +95,13 @@ struct Geo {
   static constexpr int KV = R / V;                    // upsampling windows per row part
   static constexpr bool CHUNKED = SID == 2 && UH == 1;  // 8xH: reduced rows in two halves
   static constexpr int CPOS = CHUNKED ? 32 : NOUT;    // scratch positions per chunk
+  // Scratch rows: classes with horizontal interpolation (UH > 1) keep the anchor row's left
+  // boundary sample in front of each reduced row (position k*RP, reduced (k, kx) at
+  // k*RP + kx + 1), so the interpolation reads "the sample before" without a select.
+  static constexpr bool PAD = UH > 1;
+  static constexpr int RP = PAD ? R + 1 : R;
   // scratch: [slot][PITCH] dwords; UH == 1 classes read 4 consecutive positions (16-B aligned)
-  static constexpr int PITCH = UH == 1 ? CPOS + 4 : CPOS + 1;
+  static constexpr int PITCH = UH == 1 ? CPOS + 4 : R * RP + 1;
   static constexpr int WBASE = SID == 2 ? 0 : (SID == 1 ? kWeightRowOffS1 : kWeightRowOffS0);
   static constexpr int MODES = SID == 2 ? 6 : (SID == 1 ? 8 : 16);
   static_assert(SLOTS * S * V == 64, "lanes");
@@ -258,8 +263,9 @@ struct Acc {
 // Reduced prediction of the lane's CU in the wave scratch: both modes of the pair per dword,
 // stored position (k, kx) at k*R + kx (rows offset by `k0` for the second half of a chunked
 // class).
-template <int R>
+template <int R, int RP = R>
 struct Red {
+  static constexpr int OFF = RP > R ? 1 : 0;  // padded rows: the left sample at kx = -1
   const uint32_t *p;
   int k0;
   // phase A stores floor(D) saturated at 0 only; the clip to 1023 is applied here, to
@@ -267,8 +273,9 @@ struct Red {
   static __device__ __forceinline__ s2 clip(uint32_t v) {
     return __builtin_bit_cast(s2, __builtin_elementwise_min(__builtin_bit_cast(u2, v), (u2){1023, 1023}));
   }
-  __device__ __forceinline__ s2 operator()(int k, int kx) const { return clip(p[(k + k0) * R + kx]); }
+  __device__ __forceinline__ s2 operator()(int k, int kx) const { return clip(p[(k + k0) * RP + kx + OFF]); }
   __device__ __forceinline__ void row4(int k, int kx, s2 (&out)[4]) const {  // kx % 4 == 0
+    static_assert(RP == R, "row4 reads unpadded rows");
     const uint4 v = *reinterpret_cast<const uint4 *>(p + (k + k0) * R + kx);
     out[0] = clip(v.x);
     out[1] = clip(v.y);
@@ -278,18 +285,19 @@ struct Red {
 };
 
 // Horizontal pass of anchor row k (CU row k*UV + UV-1) at strip columns x0..x0+3,
-// intra.cl:816-843; the first UH columns interpolate from the left boundary sample.
+// intra.cl:816-843; the first UH columns interpolate from the left boundary sample, which
+// the padded scratch row holds at kx = -1.
 // ((UH-o)*before + o*after + UH/2) >> LH == (base + o*delta) >> LH with
 // base = (before << LH) + UH/2; the sum equals the reference numerator, in [0, 8188].
 template <int W, int H, class RED>
-__device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, int left_k, s2 (&a)[4]) {
+__device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, s2 (&a)[4]) {
   using G = Geo<W, H>;
   if constexpr (G::UH == 1) {
     red.row4(k, x0, a);
   } else if constexpr (G::UH == 2) {
     const int kx = x0 >> 1;  // covers kx, kx+1
     const s2 r0 = red(k, kx), r1 = red(k, kx + 1);
-    const s2 before = kx == 0 ? splat(left_k) : red(k, max(kx - 1, 0));
+    const s2 before = red(k, kx - 1);
     a[0] = (before + r0 + splat(1)) >> splat(1);
     a[1] = r0;
     a[2] = (r0 + r1 + splat(1)) >> splat(1);
@@ -297,7 +305,7 @@ __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, int le
   } else {
     const int kx = x0 >> G::LH;
     const s2 after = red(k, kx);
-    const s2 before = kx == 0 ? splat(left_k) : red(k, max(kx - 1, 0));
+    const s2 before = red(k, kx - 1);
     const s2 delta = after - before;
     const s2 base = (before << splat(G::LH)) + splat(G::UH / 2);
 #pragma unroll
@@ -338,7 +346,6 @@ template <int W, int H, bool LAT, class RED>
 __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &rt, const OrigRows<H> &orig,
                                            const RED &red, int x0, int k0, int k1, s2 (&prev)[4], Acc &acc) {
   using G = Geo<W, H>;
-  auto left_at = [&](int y) { return c.left ? rt.left(c.lx - 1, c.ly + y) : c.padL; };
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
     BlockAcc b;
@@ -361,7 +368,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         s2 prow[4];
-        anchor_row<W, H>(red, 4 * by + i, x0, left_at(4 * by + i), prow);
+        anchor_row<W, H>(red, 4 * by + i, x0, prow);
         block_row(b, i, prow, orig(4 * by + i));
       }
       u2 sad, satd;
@@ -382,7 +389,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
       for (int hh = 0; hh < 2; hh++) {
         const int k = 2 * by + hh;
         s2 next[4], mid[4];
-        anchor_row<W, H>(red, k, x0, left_at(2 * k + 1), next);
+        anchor_row<W, H>(red, k, x0, next);
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) mid[cc] = as_s2((as_u2(prev[cc]) + as_u2(next[cc]) + (u2){1, 1}) >> (u2){1, 1});
         block_row(b, 2 * hh, mid, orig(2 * k));
@@ -402,7 +409,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
 #pragma unroll 1
     for (int k = k0; k < k1; k++) {
       s2 next[4];
-      anchor_row<W, H>(red, k, x0, left_at(k * G::UV + G::UV - 1), next);
+      anchor_row<W, H>(red, k, x0, next);
       u2 delta[4], base[4];
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) {
@@ -477,8 +484,10 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   constexpr int NCS = (G::SLOTS + 7) / 8;  // column sets (8 CUs x 2 modes) of a full task
   constexpr int NRB = G::CPOS / 16;        // 16-row blocks in this chunk
   // the lane's 4 results of block rb sit at stored positions pos0 + i * PSTEP
-  constexpr int PSTEP = G::SID == 2 ? (TR ? 8 : 1) : (TR ? 4 : 1);
-  uint8_t *lane_dst = x.wave + kCuTableBytes + ((r >> 1) * G::PITCH + (TR ? h : 4 * h)) * 4 + 2 * (r & 1);
+  // (padded rows: position (k, kx) at k*RP + kx + 1; outputs 4h..4h+3 share one row)
+  constexpr int PSTEP = TR ? G::RP : 1;
+  const int pos0 = TR ? h + G::PAD : (G::PAD ? (4 * h / G::R) * G::RP + (4 * h) % G::R + 1 : 4 * h);
+  uint8_t *lane_dst = x.wave + kCuTableBytes + ((r >> 1) * G::PITCH + pos0) * 4 + 2 * (r & 1);
 #pragma unroll
   for (int rb = 0; rb < NRB; rb++) {
     int jofs, pofs;  // uniform: matrix row offset, stored-position offset of the block
@@ -487,11 +496,11 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
       const int cofs = G::CHUNKED ? 32 * chunk : 0;
       if constexpr (!TR) {
         jofs = 16 * rbg;
-        pofs = 16 * rbg - cofs;
+        pofs = G::PAD ? 2 * rbg * G::RP : 16 * rbg - cofs;
       } else {  // output j = 8*(h + 4*rr) + i + 4*cc -> position (i + 4cc, h + 4rr)
         const int cc = rbg >> 1, rr = rbg & 1;
         jofs = 32 * rr + 4 * cc;
-        pofs = 32 * cc + 4 * rr - cofs;
+        pofs = G::PAD ? 4 * cc * G::RP + 4 * rr : 32 * cc + 4 * rr - cofs;
       }
     } else {
       jofs = 0;
@@ -568,13 +577,22 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   orig.load(x.org, c.lx + x0, c.ly);
   const size_t cbase = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
   const uint32_t *mine = reinterpret_cast<const uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
-  const Red<G::R> red{mine, 0};
+  const Red<G::R, G::RP> red{mine, 0};
   s2 top[4];  // top boundary of the strip: upsampling state above window 0
   {
     const uint2 tv = rt.top4(c.lx + x0, c.ly - 1);
     const int t4[4] = {(int)(tv.x & 0xffff), (int)(tv.x >> 16), (int)(tv.y & 0xffff), (int)(tv.y >> 16)};
 #pragma unroll
     for (int cc = 0; cc < 4; cc++) top[cc] = splat(c.top ? t4[cc] : c.padT);
+  }
+  if constexpr (G::PAD) {
+    // left boundary sample of anchor row k (CU row k*UV + UV - 1), both halves; phase A
+    // never writes these positions
+    uint32_t *lcol = reinterpret_cast<uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
+    for (int k = sub; k < G::R; k += G::S * G::V) {
+      const uint32_t lv = c.left ? rt.left(c.lx - 1, c.ly + k * G::UV + G::UV - 1) : c.padL;
+      if (active) lcol[k * G::RP] = lv | lv << 16;
+    }
   }
   wave_lds_sync();
 
@@ -591,7 +609,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       wave_lds_sync();
       phase_a<W, H>(x, lane, ncu, q, 1);
       wave_lds_sync();
-      const Red<G::R> red_hi{mine, -4};  // chunk 1 holds reduced rows 4..7
+      const Red<G::R, G::RP> red_hi{mine, -4};  // chunk 1 holds reduced rows 4..7
       walk_strip<W, H>(c, rt, orig, red_hi, x0, 4, 8, prev, acc);  // prev carries anchor row 3
     } else if constexpr (G::SID == 0) {
       walk_strip<W, H>(c, rt, orig, red, x0, 0, 4, prev, acc);
@@ -599,7 +617,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       // row part v: windows [v*KV, (v+1)*KV) (rows when UV == 1)
       const int k0 = G::V > 1 ? v * G::KV : 0;
       if constexpr (G::V > 1 && G::UV > 1) {
-        if (k0 > 0) anchor_row<W, H>(red, k0 - 1, x0, c.left ? rt.left(c.lx - 1, c.ly + k0 * G::UV - 1) : c.padL, prev);
+        if (k0 > 0) anchor_row<W, H>(red, k0 - 1, x0, prev);
       }
       walk_strip<W, H>(c, rt, orig, red, x0, k0, k0 + G::KV, prev, acc);
     }
