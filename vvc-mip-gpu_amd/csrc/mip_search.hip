@@ -28,6 +28,8 @@
 // pinned to the reference kernels' own outputs (tests/golden/).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 
 #include "mip_kernels.h"
 #include "mip_tables.h"
@@ -72,6 +74,43 @@ __device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_ma
 __device__ __forceinline__ s2 smin(s2 a, s2 b) { return __builtin_elementwise_min(a, b); }
 
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
+
+// (a + b + 1) >> 1 on both halves of non-negative 10-bit samples: one 32-bit three-input add
+// (a + b + 1 <= 2047, so no carry crosses the halves) and one packed shift.
+__device__ __forceinline__ s2 avg_round(s2 a, s2 b) {
+  const uint32_t t = __builtin_bit_cast(uint32_t, a) + __builtin_bit_cast(uint32_t, b) + 0x00010001u;
+  return __builtin_bit_cast(s2, __builtin_bit_cast(u2, t) >> (u2){1, 1});
+}
+
+// Compile-time loop: f(integral_constant<int, I>) for I = 0..N-1.
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F &f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// a * O + c on both 16-bit halves as ONE v_pk_mad_u16 (the compiler splits small constant
+// multipliers into shift + add).
+template <int O>
+__device__ __forceinline__ u2 pk_mad_c(u2 a, u2 c) {
+  if constexpr (O == 1) {
+    return a + c;
+  } else {
+    u2 d;
+    asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "i"(O), "v"(c));
+    return d;
+  }
+}
+// a * O + C on both halves, O and C constants
+template <int O, int C>
+__device__ __forceinline__ u2 pk_mad_cc(u2 a) {
+  u2 d;
+  asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(a), "i"(O), "i"(C));
+  return d;
+}
 
 // LDS fence for data handed between lanes of ONE wave (wave-private scratch).
 __device__ __forceinline__ void wave_lds_sync() {
@@ -298,21 +337,32 @@ __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, s2 (&a
     const int kx = x0 >> 1;  // covers kx, kx+1
     const s2 r0 = red(k, kx), r1 = red(k, kx + 1);
     const s2 before = red(k, kx - 1);
-    a[0] = (before + r0 + splat(1)) >> splat(1);
+    a[0] = avg_round(before, r0);
     a[1] = r0;
-    a[2] = (r0 + r1 + splat(1)) >> splat(1);
+    a[2] = avg_round(r0, r1);
     a[3] = r1;
   } else {
     const int kx = x0 >> G::LH;
     const s2 after = red(k, kx);
     const s2 before = red(k, kx - 1);
-    const s2 delta = after - before;
-    const s2 base = (before << splat(G::LH)) + splat(G::UH / 2);
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int o = ((x0 + c) & (G::UH - 1)) + 1;
-      a[c] = (splat(o) * delta + base) >> splat(G::LH);
-    }
+    const u2 delta = as_u2(after - before);
+    const u2 base = pk_mad_cc<G::UH, G::UH / 2>(as_u2(before));
+    // the strip's 4 columns are phases o0+1..o0+4 of one window (o0 = 0 or 4 for UH = 8)
+    const int o0 = x0 & (G::UH - 1);
+    auto tap = [&](auto oc) {  // (o*delta + base) >> LH, o = oc + 1 + o0
+      constexpr int c = decltype(oc)::value;
+      if constexpr (G::UH == 4) {
+        if constexpr (c == 3) return after;  // o = UH: the anchor itself
+        else return as_s2(pk_mad_c<c + 1>(delta, base) >> (u2){G::LH, G::LH});
+      } else {
+        const u2 v = o0 == 0 ? pk_mad_c<c + 1>(delta, base) : pk_mad_c<c + 5>(delta, base);
+        return as_s2(v >> (u2){G::LH, G::LH});
+      }
+    };
+    a[0] = tap(std::integral_constant<int, 0>{});
+    a[1] = tap(std::integral_constant<int, 1>{});
+    a[2] = tap(std::integral_constant<int, 2>{});
+    a[3] = tap(std::integral_constant<int, 3>{});
   }
 }
 
@@ -391,7 +441,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
         s2 next[4], mid[4];
         anchor_row<W, H>(red, k, x0, next);
 #pragma unroll
-        for (int cc = 0; cc < 4; cc++) mid[cc] = as_s2((as_u2(prev[cc]) + as_u2(next[cc]) + (u2){1, 1}) >> (u2){1, 1});
+        for (int cc = 0; cc < 4; cc++) mid[cc] = avg_round(prev[cc], next[cc]);
         block_row(b, 2 * hh, mid, orig(2 * k));
         block_row(b, 2 * hh + 1, next, orig(2 * k + 1));
 #pragma unroll
@@ -414,24 +464,25 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) {
         delta[cc] = as_u2(next[cc]) - as_u2(prev[cc]);
-        base[cc] = as_u2(prev[cc]) * (u2){G::UV, G::UV} + (u2){G::UV / 2, G::UV / 2};
+        base[cc] = pk_mad_cc<G::UV, G::UV / 2>(as_u2(prev[cc]));
       }
-#pragma unroll
-      for (int bi = 0; bi < NB; bi++) {
+      static_for<NB>([&](auto bi_c) {
+        constexpr int bi = decltype(bi_c)::value;
         BlockAcc b;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const unsigned short o = (unsigned short)(4 * bi + i + 1);
+        static_for<4>([&](auto i_c) {
+          constexpr int i = decltype(i_c)::value, o = 4 * bi + i + 1;
           s2 prow[4];
 #pragma unroll
-          for (int cc = 0; cc < 4; cc++)
-            prow[cc] = o == G::UV ? next[cc] : as_s2(((u2){o, o} * delta[cc] + base[cc]) >> (u2){G::LV, G::LV});
+          for (int cc = 0; cc < 4; cc++) {
+            if constexpr (o == G::UV) prow[cc] = next[cc];
+            else prow[cc] = as_s2(pk_mad_c<o>(delta[cc], base[cc]) >> (u2){G::LV, G::LV});
+          }
           block_row(b, i, prow, orig(k * G::UV + 4 * bi + i));
-        }
+        });
         u2 sad, satd;
         block_finish(b, sad, satd);
         acc.add(sad, satd);
-      }
+      });
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
     }
