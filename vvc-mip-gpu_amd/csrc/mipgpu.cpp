@@ -133,6 +133,12 @@ double cut_factor() {
   return e && atof(e) > 0 ? atof(e) : 2.0;
 }
 
+// MIPGPU_NO_PAIRS=1 (profiling knob): tasks keep their prologue but search no mode pair.
+bool no_pairs() {
+  const char *e = getenv("MIPGPU_NO_PAIRS");
+  return e && *e == '1';
+}
+
 // Estimated VALU instructions per lane for one mode pair of a task of `ncu` CUs.
 double pair_cost(int cls, int ncu) {
   const int w = mipgpu::kClassW[cls], h = mipgpu::kClassH[cls];
@@ -199,6 +205,7 @@ WorkLists build_work(int slices, int waves, int width, int height) {
         c.t.q0 = (uint8_t)(p.t.q0 + np * i / parts);
         c.t.q1 = (uint8_t)(p.t.q0 + np * (i + 1) / parts);
         c.cost = p.cost * (c.t.q1 - c.t.q0) + 150.0;
+        if (no_pairs()) c.t.q1 = c.t.q0;  // profiling: task prologues only
         cut.push_back(c);
       }
     }
