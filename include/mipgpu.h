@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MIPGPU_ABI_VERSION 2
+#define MIPGPU_ABI_VERSION 3
 #define MIP_COSTS_PER_CTU_ABI 97840
 #define MIP_CUS_PER_CTU_ABI 5380
 #define MIP_COST_UNAVAILABLE 0x7fffffff
@@ -56,6 +56,8 @@ typedef struct {
   int want_sad_satd;   /* also produce the SAD / SATD tables (MAX_PERFORMANCE_DIST=0) */
   int slices_per_ctu;  /* workgroups per 64x64 CTU quadrant in the search kernel; 0 = auto
                           (chosen per launch: more, smaller workgroups for small batches) */
+  int best_k;          /* decision list length K of best_mode_out / best_cost_out (1..32;
+                          0 = 1): the K lowest-cost modes of every CU, see mip_topk_device */
 } mip_opts;
 
 typedef struct mip_engine mip_engine;
@@ -91,8 +93,9 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
  * refs_or_null: caller-provided reference-sample frames (alternative samples computed
  * elsewhere); NULL = originals, or the engine's filter when opts.filter != NONE.
  * costs_out: int32 [nframes][nCTUs*97840] (may be NULL if only best modes are wanted).
- * best_mode_out / best_cost_out: optional per-CU argmin, [nframes][nCTUs*5380]
- * (0xff / MIP_COST_UNAVAILABLE for unavailable CUs).
+ * best_mode_out / best_cost_out: optional per-CU decision lists, [nframes][nCTUs*5380][K]
+ * with K = opts.best_k (K = 1: the argmin; mip_topk_device gives the ordering rules;
+ * 0xff / MIP_COST_UNAVAILABLE for unavailable CUs).
  * sad_out / satd_out: optional (need opts.want_sad_satd).  Synchronous. */
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
                       int nframes, int32_t *costs_out, uint8_t *best_mode_out,
@@ -106,6 +109,17 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
 int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
                       int nframes, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
                       uint8_t *d_best_mode, int32_t *d_best_cost, void *stream);
+
+/* Per-CU decision lists (no reference counterpart; what an encoder's full-RD stage takes
+ * from the cost table, e.g. VTM's numModesForFullRD MIP candidates): for every CU of
+ * `nframes` device cost tables (reference layout), the k lowest-cost modes in increasing
+ * cost order, ties to the lower mode index.  Modes are numbered as the log's Mode column
+ * (0..2*modes-1, transposed modes >= modes).  Entries past the CU's 2*modes modes and all
+ * entries of unavailable CUs are 0xff / MIP_COST_UNAVAILABLE.  k in 1..32.
+ * d_modes: uint8 [nframes][nCTUs*5380][k]; d_costs_k: int32, same shape (either may be
+ * NULL).  Asynchronous on `stream`. */
+int mip_topk_device(const int32_t *d_costs, int width, int height, int nframes, int k,
+                    uint8_t *d_modes, int32_t *d_costs_k, void *stream);
 
 /* Device-resident filter (asynchronous on `stream`). */
 int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int height,

@@ -92,6 +92,15 @@ def test_unknown_and_ambiguous_options():
     assert "ambiguous" in run(["--F", "1"]).stderr  # FramesToBeEncoded / FilterType
 
 
+@needs_cli
+def test_extension_arguments_are_validated():
+    for bad in (["--TopK", "0"], ["--TopK", "33"], ["--InputFormat", "rgb"], ["--TopK", "x"]):
+        r = run(["-f", "1", "-s", "128x128", "-o", "x.csv"] + bad)
+        assert r.returncode == 1 and "is invalid" in r.stderr, bad
+    r = run(["-h"])
+    assert all(k in r.stdout for k in ("--TopK", "--BinaryLog", "--InputFormat"))
+
+
 # ------------------------------------------------------------ GPU: the cost log
 @pytest.mark.gpu
 @needs_cli
@@ -142,3 +151,55 @@ def test_cost_log_is_byte_identical(gpu_available, tmp_path, extra, filt, kidx, 
     got = open(prefix + ".csv", "rb").read()
     want = reference_log(cost, W, sad, satd)
     assert len(got) == len(want) and got == want
+
+
+@pytest.mark.gpu
+@needs_cli
+def test_raw_inputs_binary_log_and_topk(gpu_available, tmp_path):
+    """--InputFormat u16 / yuv420p10 (luma plane) give the CSV input's log; --BinaryLog holds
+    every frame's cost table; --TopK 4 lists each CU's 4 best modes in rank order."""
+    W, H, N, K = 264, 136, 2, 4
+    frames = synth_frames(W, H, N, 0xC13, 0)
+    write_csv(tmp_path / "in.csv", frames)
+    frames.astype("<u2").tofile(tmp_path / "in.u16")
+    rng = np.random.default_rng(3)
+    with open(tmp_path / "in.yuv", "wb") as f:
+        for fr in frames:
+            f.write(fr.astype("<u2").tobytes())
+            f.write(rng.integers(0, 1024, size=2 * (W // 2) * (H // 2), dtype=np.uint16).astype("<u2").tobytes())
+    logs = {}
+    for name, extra in (("csv", []), ("u16", []), ("yuv", ["--InputFormat", "yuv420p10"])):
+        prefix = str(tmp_path / ("out_" + name))
+        r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / ("in." + name)), "-l", prefix,
+                 "--BinaryLog", prefix + ".bin", "--BestModes", prefix + "_best.csv", "--TopK", str(K)] + extra)
+        assert r.returncode == 0, r.stdout + r.stderr
+        logs[name] = open(prefix + ".csv", "rb").read()
+    assert logs["csv"] == logs["u16"] == logs["yuv"]
+    want = [mask_unavailable(O.search(frames[f]), W, H) for f in range(N)]
+    b = layout.read_binary_log(str(tmp_path / "out_yuv.bin"))
+    assert (b["width"], b["height"], b["frames"]) == (W, H, N) and "sad" not in b
+    assert np.array_equal(np.asarray(b["cost"]), np.stack(want))
+    # decision lists: rows of the BestModes CSV vs the numpy statement
+    import csv
+    rows = list(csv.DictReader(open(tmp_path / "out_yuv_best.csv")))
+    n = layout.num_ctus(W, H)
+    got = {}
+    for r in rows:
+        got.setdefault((int(r["Frame"]), int(r["CTU"]), r["cuSizeName"], int(r["CU"])), []).append(
+            (int(r["Rank"]), int(r["Mode"]), int(r["Transposed"]), int(r["Cost"])))
+    shapes = {s.name: s for s in layout.SHAPES}
+    for f in range(N):
+        wm, wc = layout.topk_modes(want[f], n, K)
+        k = 0
+        for ctu in range(n):
+            for s in layout.SHAPES:
+                for cu in range(s.ncu):
+                    lst = got[(f, ctu, s.name, cu)]
+                    if wm[k, 0] == 0xFF:
+                        assert lst == [(0, -1, -1, layout.UNAVAILABLE)]
+                    else:
+                        exp = [(r, int(m) % s.modes, int(m >= s.modes), int(c))
+                               for r, (m, c) in enumerate(zip(wm[k], wc[k])) if m != 0xFF]
+                        assert lst == exp
+                    k += 1
+    assert set(shapes) == {key[2] for key in got}

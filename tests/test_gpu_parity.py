@@ -137,6 +137,33 @@ def test_many_launches_on_two_streams(gpu_available):
             assert np.array_equal(c.cpu().numpy(), want[:n])
 
 
+@pytest.mark.parametrize("k", [1, 3, 13, 32])
+def test_topk_decision_lists(gpu_available, k):
+    """mip_topk_device / engine best_k vs the numpy statement on oracle cost tables (edge
+    CTUs: unavailable CUs; k = 13 and 32 exceed the 12 / 16 modes of some shapes)."""
+    import torch
+    from mipgpu import topk_device
+    w, h = 264, 136
+    frames = synth_frames(w, h, 2, 0x7C, 0)
+    want = [O.search(frames[f]) for f in range(2)]
+    n = layout.num_ctus(w, h)
+    d = torch.from_numpy(np.stack(want)).cuda()
+    modes, costs = topk_device(d, w, h, k)
+    torch.cuda.synchronize()
+    with MipEngine(w, h, max_batch=2, best_k=k) as eng:
+        out = eng.search(frames, best=True)
+    for f in range(2):
+        wm, wc = layout.topk_modes(want[f], n, k)
+        assert np.array_equal(modes[f].cpu().numpy(), wm)
+        assert np.array_equal(costs[f].cpu().numpy(), wc)
+        em = out["best_mode"][f].reshape(-1, k)
+        ec = out["best_cost"][f].reshape(-1, k)
+        assert np.array_equal(em, wm) and np.array_equal(ec, wc)
+    if k == 1:
+        bm, bc = layout.best_modes(want[0], n)
+        assert np.array_equal(modes[0, :, 0].cpu().numpy(), bm)
+
+
 def test_errors_are_loud(gpu_available):
     with pytest.raises(MipError):
         MipEngine(130, 64)  # width not a multiple of 4
@@ -144,6 +171,8 @@ def test_errors_are_loud(gpu_available):
         MipEngine(128, 64, filter="filterFrame_2d_int_quarterCtu", kernel_idx=7)
     with pytest.raises(MipError):
         filter_index("filterFrame_2d_float")  # not whitelisted
+    with pytest.raises(MipError):
+        MipEngine(128, 64, best_k=33)
 
 
 def _extreme(pattern, w, h):

@@ -43,6 +43,24 @@ def test_best_modes_numpy():
 
 
 @pytest.mark.skipif(not HAVE_REF, reason="reference tree not mounted")
+def test_topk_numpy_statement():
+    """layout.topk_modes: stable ordering, padding past a CU's modes, unavailable CUs."""
+    rng = np.random.default_rng(5)
+    c = rng.integers(0, 50, size=2 * layout.COSTS_PER_CTU).astype(np.int32)  # many ties
+    c[layout.COSTS_PER_CTU:layout.COSTS_PER_CTU + 12] = layout.UNAVAILABLE   # CU 0 of CTU 1
+    m1, v1 = layout.topk_modes(c, 2, 1)
+    bm, bv = layout.best_modes(c, 2)
+    assert np.array_equal(m1[:, 0], bm) and np.array_equal(v1[:, 0], bv)
+    m, v = layout.topk_modes(c, 2, 32)
+    s0 = layout.SHAPES[0]
+    row = c[:2 * s0.modes]
+    want = sorted(range(len(row)), key=lambda i: (row[i], i))
+    assert list(m[0, :len(row)]) == want and list(v[0, :len(row)]) == [row[i] for i in want]
+    assert (m[0, len(row):] == 0xFF).all() and (v[0, len(row):] == layout.UNAVAILABLE).all()
+    assert (m[layout.CUS_PER_CTU] == 0xFF).all() and (v[layout.CUS_PER_CTU] == layout.UNAVAILABLE).all()
+    assert (np.diff(v[:, :12].astype(np.int64), axis=1) >= 0).all()
+
+
 def test_generated_header_matches_reference():
     """Re-derive the tables from the reference files and compare with the committed ones."""
     sys.path.insert(0, TOOLS)

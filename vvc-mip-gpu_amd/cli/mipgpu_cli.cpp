@@ -14,6 +14,10 @@
 // practice); this CLI prints 0 there too unless --ReportSadSatd is given.
 // Extensions: --ReportSadSatd, --AllFrames (log every frame, column CTU stays per frame,
 // a Frame column is NOT added to keep the format), --BestModes file (per-CU decision),
+// --TopK K (the BestModes file lists each CU's K best modes, one row per rank),
+// --BinaryLog file (every frame's int32 cost table, mipgpu/layout.py read_binary_log),
+// --InputFormat csv|u16|yuv420p10 (raw little-endian 16-bit luma frames, or planar
+// 4:2:0 10-bit YUV of which the luma plane is used; auto: by file extension),
 // --BatchFrames N, --Threads N (log formatting threads), and --DeviceIndex accepting a
 // list ("0,1,2,3"): the frames are sharded over those GPUs, one engine and one host thread
 // per device (frames are independent; no inter-GPU communication).
@@ -39,12 +43,12 @@ const char *kFilters[] = {"filterFrame_1d_int", "filterFrame_1d_float", "filterF
                           "filterFrame_2d_int_5x5_quarterCtu", "filterFrame_2d_float_5x5_quarterCtu"};
 
 struct Options {
-  int frames = -1, kernel_idx = 0, batch = 8, threads = 0;
+  int frames = -1, kernel_idx = 0, batch = 8, threads = 0, topk = 1;
   std::vector<int> devices{0};
   std::string device_arg = "0";
   bool device_set = false, prefix_set = false, kidx_set = false, help = false;
   bool sad_satd = false, all_frames = false;
-  std::string resolution, input, prefix, filter, best_modes;
+  std::string resolution, input, prefix, filter, best_modes, binary_log, input_format = "auto";
 };
 
 struct OptDef {
@@ -56,7 +60,8 @@ const OptDef kOpts[] = {{"help", 'h', false},        {"DeviceIndex", 0, true},  
                         {"Resolution", 's', true},   {"OriginalFrames", 'o', true}, {"OutputPreffix", 'l', true},
                         {"FilterType", 0, true},     {"KernelIdx", 0, true},     {"ReportSadSatd", 0, false},
                         {"AllFrames", 0, false},     {"BestModes", 0, true},     {"BatchFrames", 0, true},
-                        {"Threads", 0, true}};
+                        {"Threads", 0, true},        {"TopK", 0, true},          {"BinaryLog", 0, true},
+                        {"InputFormat", 0, true}};
 
 void usage() {
   std::cout << "Allowed options:\n"
@@ -72,7 +77,10 @@ void usage() {
                "  --AllFrames                       Log every frame (reference logs frame 0 only)\n"
                "  --BestModes arg                   Write the per-CU best mode / cost to this CSV\n"
                "  --BatchFrames arg (=8)            Frames per device batch\n"
-               "  --Threads arg (=0)                Log-formatting threads (0 = all cores)\n";
+               "  --Threads arg (=0)                Log-formatting threads (0 = all cores)\n"
+               "  --TopK arg (=1)                   Modes per CU in the BestModes file (1..32, ranked)\n"
+               "  --BinaryLog arg                   Write every frame's int32 cost table to this file\n"
+               "  --InputFormat arg (=auto)         csv | u16 (raw 16-bit luma) | yuv420p10 (planar 4:2:0, 10 bit)\n";
 }
 
 int set_opt(Options &o, const std::string &name, const std::string &val) {
@@ -98,6 +106,15 @@ int set_opt(Options &o, const std::string &name, const std::string &val) {
     else if (name == "BestModes") o.best_modes = val;
     else if (name == "BatchFrames") o.batch = std::max(1, std::stoi(val));
     else if (name == "Threads") o.threads = std::stoi(val);
+    else if (name == "TopK") {
+      o.topk = std::stoi(val);
+      if (o.topk < 1 || o.topk > 32) throw std::invalid_argument("TopK");
+    }
+    else if (name == "BinaryLog") o.binary_log = val;
+    else if (name == "InputFormat") {
+      if (val != "auto" && val != "csv" && val != "u16" && val != "yuv420p10") throw std::invalid_argument("format");
+      o.input_format = val;
+    }
   } catch (...) {
     std::cerr << "the argument ('" << val << "') for option '--" << name << "' is invalid\n";
     return 1;
@@ -206,6 +223,32 @@ bool read_frames(const std::string &path, int W, int H, int n, uint16_t *out) {
   return true;
 }
 
+// Raw frames: `luma_only` = consecutive W x H little-endian 16-bit frames; otherwise planar
+// 4:2:0 with 16-bit samples (yuv420p10le), whose two chroma planes (W/2 x H/2 each) are skipped.
+bool read_raw_frames(const std::string &path, int W, int H, int n, bool luma_only, uint16_t *out) {
+  FILE *f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  const size_t fs = (size_t)W * H, chroma = luma_only ? 0 : 2 * (size_t)(W / 2) * (H / 2);
+  bool ok = true;
+  for (int i = 0; i < n && ok; i++) {
+    ok = fread(out + i * fs, 2, fs, f) == fs;
+    if (ok && chroma) ok = fseek(f, (long)(chroma * 2), SEEK_CUR) == 0;
+  }
+  fclose(f);
+  return ok;
+}
+
+std::string input_format(const Options &o) {
+  if (o.input_format != "auto") return o.input_format;
+  auto ends = [&](const char *suf) {
+    const size_t n = strlen(suf);
+    return o.input.size() >= n && o.input.compare(o.input.size() - n, n, suf) == 0;
+  };
+  if (ends(".yuv")) return "yuv420p10";
+  if (ends(".u16") || ends(".raw")) return "u16";
+  return "csv";
+}
+
 inline char *put_int(char *p, long long v) {
   char tmp[24];
   int n = 0;
@@ -297,7 +340,10 @@ int main(int argc, char **argv) {
     std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
     return 1;
   }
-  if (!read_frames(o.input, W, H, o.frames, frames.data())) {
+  const std::string fmt = input_format(o);
+  const bool read_ok = fmt == "csv" ? read_frames(o.input, W, H, o.frames, frames.data())
+                                    : read_raw_frames(o.input, W, H, o.frames, fmt == "u16", frames.data());
+  if (!read_ok) {
     perror("error while opening samples files");
     return 1;
   }
@@ -308,6 +354,7 @@ int main(int argc, char **argv) {
   opts.kernel_idx = o.kernel_idx;
   opts.max_batch = std::min(o.batch, std::max(1, o.frames));
   opts.want_sad_satd = o.sad_satd ? 1 : 0;
+  opts.best_k = o.topk;
   std::vector<mip_engine *> engines;
   auto destroy_all = [&]() {
     for (mip_engine *e : engines) mip_engine_destroy(e);
@@ -322,7 +369,7 @@ int main(int argc, char **argv) {
     }
     engines.push_back(e);
   }
-  const size_t cpf = (size_t)nctus * MIP_COSTS_PER_CTU_ABI, upf = (size_t)nctus * MIP_CUS_PER_CTU_ABI;
+  const size_t cpf = (size_t)nctus * MIP_COSTS_PER_CTU_ABI, upf = (size_t)nctus * MIP_CUS_PER_CTU_ABI * o.topk;
   Pinned<int32_t> cost, sad, satd, best_cost;
   Pinned<uint8_t> best;
   bool ok = cost.alloc(cpf * o.frames);
@@ -389,19 +436,42 @@ int main(int argc, char **argv) {
   if (!o.best_modes.empty()) {
     FILE *fp = fopen(o.best_modes.c_str(), "w");
     if (!fp) { perror("cannot open best-mode file"); destroy_all(); return 1; }
-    fprintf(fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,Transposed,Cost\n");
+    const int K = o.topk;
+    if (K == 1) fprintf(fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,Transposed,Cost\n");
+    else fprintf(fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,Rank,Mode,Transposed,Cost\n");
     const int ctu_cols = (W + 127) / 128;
     for (int f = 0; f < o.frames; f++)
       for (int ctu = 0, k = 0; ctu < nctus; ctu++)
         for (const ShapeInfo &sh : shapes)
           for (int cu = 0; cu < sh.ncu; cu++, k++) {
-            const size_t i = f * upf + (size_t)ctu * MIP_CUS_PER_CTU_ABI + (k % MIP_CUS_PER_CTU_ABI);
-            const int m = best[i];
-            fprintf(fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu,
-                    128 * (ctu % ctu_cols) + sh.x[cu], 128 * (ctu / ctu_cols) + sh.y[cu], m == 0xff ? -1 : m % sh.modes,
-                    m == 0xff ? -1 : (m >= sh.modes), best_cost[i]);
+            const size_t i0 = f * upf + ((size_t)ctu * MIP_CUS_PER_CTU_ABI + (k % MIP_CUS_PER_CTU_ABI)) * K;
+            const int x = 128 * (ctu % ctu_cols) + sh.x[cu], y = 128 * (ctu / ctu_cols) + sh.y[cu];
+            for (int r = 0; r < K; r++) {
+              const int m = best[i0 + r];
+              if (K > 1 && m == 0xff && best[i0] != 0xff) break;  // past the CU's modes
+              if (K == 1)
+                fprintf(fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x, y,
+                        m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
+              else
+                fprintf(fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x, y, r,
+                        m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
+              if (m == 0xff) break;  // unavailable CU: one row
+            }
           }
     fclose(fp);
+  }
+  if (!o.binary_log.empty()) {
+    // header: "MIPC", version 1, width, height, frames, entries per frame, flags (bit 0: SAD
+    // and SATD tables follow the cost tables), reserved; then int32 little-endian tables
+    FILE *fp = fopen(o.binary_log.c_str(), "wb");
+    if (!fp) { perror("cannot open binary log"); destroy_all(); return 1; }
+    const uint32_t hdr[8] = {0x4350494du, 1u, (uint32_t)W, (uint32_t)H, (uint32_t)o.frames, (uint32_t)cpf,
+                             o.sad_satd ? 1u : 0u, 0u};
+    bool wok = fwrite(hdr, 4, 8, fp) == 8 && fwrite(cost.data(), 4, cpf * o.frames, fp) == cpf * o.frames;
+    if (o.sad_satd)
+      wok = wok && fwrite(sad.data(), 4, cpf * o.frames, fp) == cpf * o.frames &&
+            fwrite(satd.data(), 4, cpf * o.frames, fp) == cpf * o.frames;
+    if (fclose(fp) != 0 || !wok) { perror("writing binary log"); destroy_all(); return 1; }
   }
   const long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count();
   printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n");

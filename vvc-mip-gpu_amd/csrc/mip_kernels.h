@@ -90,10 +90,12 @@ constexpr int kTableBytes = kWeightRows * 16 + kCtabRows * 4;
 
 struct BestArgs {
   const int32_t *cost;
-  uint8_t *best_mode;
-  int32_t *best_cost;
+  uint8_t *best_mode;     // [total_cus][k]
+  int32_t *best_cost;     // [total_cus][k]
   int total_cus;          // frames * nctus * 5380
+  int k;                  // decision list length, 1..kMaxBestK
 };
+constexpr int kMaxBestK = 32;
 
 struct FilterArgs {
   const uint16_t *in;

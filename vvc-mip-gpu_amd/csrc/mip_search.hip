@@ -824,7 +824,33 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   }
 }
 
-// Per-CU argmin over the cost row (lowest mode wins ties); 0xff for unavailable CUs.
+// Decision list of one CU: the k lowest-cost of its M modes (ties to the lower mode), by
+// repeated selection over the row held in registers; 0xff / kUnavailable past the M modes
+// and for unavailable CUs (every entry of such a row is kUnavailable).
+template <int M>
+__device__ __forceinline__ void topk_row(const int32_t *row, int k, uint8_t *mo, int32_t *co) {
+  int v[M];
+#pragma unroll
+  for (int m = 0; m < M; m += 4) {  // rows start 16-byte aligned (12, 16 or 32 entries per CU)
+    const int4 q = *reinterpret_cast<const int4 *>(row + m);
+    v[m] = q.x, v[m + 1] = q.y, v[m + 2] = q.z, v[m + 3] = q.w;
+  }
+  const bool unavailable = v[0] == kUnavailable;
+  uint32_t used = 0;
+  for (int r = 0; r < k; r++) {
+    int best = 0, bc = 0;
+    bool found = false;
+#pragma unroll
+    for (int m = 0; m < M; m++)
+      if (!((used >> m) & 1) && (!found || v[m] < bc)) best = m, bc = v[m], found = true;
+    const bool ok = found && !unavailable;
+    if (ok) used |= 1u << best;
+    if (mo) mo[r] = ok ? (uint8_t)best : 0xff;
+    if (co) co[r] = ok ? bc : kUnavailable;
+  }
+}
+
+// Per-CU decision lists (k = 1: the argmin).
 __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= a.total_cus) return;
@@ -833,11 +859,13 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
   while (r >= c_shapes[s].ncu) r -= c_shapes[s++].ncu;
   const mip_shape_desc sd = c_shapes[s];
   const int32_t *row = a.cost + (size_t)ctu * MIP_COSTS_PER_CTU + sd.cost_offset + (size_t)r * 2 * sd.modes;
-  int best = 0, bc = row[0];
-  for (int m = 1; m < 2 * sd.modes; m++)
-    if (row[m] < bc) bc = row[m], best = m;
-  if (a.best_mode) a.best_mode[g] = bc == kUnavailable ? 0xff : (uint8_t)best;
-  if (a.best_cost) a.best_cost[g] = bc;
+  uint8_t *mo = a.best_mode ? a.best_mode + (size_t)g * a.k : nullptr;
+  int32_t *co = a.best_cost ? a.best_cost + (size_t)g * a.k : nullptr;
+  switch (sd.modes) {
+    case 6: topk_row<12>(row, a.k, mo, co); break;
+    case 8: topk_row<16>(row, a.k, mo, co); break;
+    default: topk_row<32>(row, a.k, mo, co); break;
+  }
 }
 
 }  // namespace
@@ -884,6 +912,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, hip
 }
 
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s) {
+  if (a.k < 1 || a.k > kMaxBestK) return hipErrorInvalidValue;
   hipLaunchKernelGGL(best_mode_kernel, dim3((a.total_cus + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }

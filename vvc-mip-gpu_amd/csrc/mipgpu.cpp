@@ -288,6 +288,7 @@ void mip_opts_default(mip_opts *o) {
   o->max_batch = 1;
   o->want_sad_satd = 0;
   o->slices_per_ctu = 0;
+  o->best_k = 1;
 }
 
 const char *mip_last_error(void) { return g_err.c_str(); }
@@ -350,6 +351,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   mip_opts_default(&o);
   if (opts) o = *opts;
   if (o.max_batch < 1) return fail("max_batch must be >= 1");
+  if (o.best_k == 0) o.best_k = 1;
+  if (o.best_k < 1 || o.best_k > mipgpu::kMaxBestK) return fail("best_k %d out of range 1..%d", o.best_k, mipgpu::kMaxBestK);
   if (o.filter != MIP_FILTER_NONE) {
     if (!filter_valid(o.filter, o.kernel_idx)) return fail("invalid filter %d / kernel_idx %d", o.filter, o.kernel_idx);
   }
@@ -383,13 +386,13 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     ALLOC(e->d_sad, ncost * 4);
     ALLOC(e->d_satd, ncost * 4);
   }
-  ALLOC(e->d_best, ncu);
+  ALLOC(e->d_best, ncu * o.best_k);
   ALLOC(e->d_queue, 2 * mip_engine::kQueueSlots * sizeof(uint32_t));
   if (hipMemset(e->d_queue, 0, 2 * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail("hipMemset failed"));
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
-  ALLOC(e->d_best_cost, ncu * 4);
+  ALLOC(e->d_best_cost, ncu * o.best_k * 4);
   std::vector<int> slice_set;
   if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
   else slice_set = {1, 2, 4};
@@ -420,6 +423,18 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   if (hipMemcpy(e->d_tables, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail("uploading static tables failed"));
   *out = e;
+  return 0;
+}
+
+int mip_topk_device(const int32_t *d_costs, int width, int height, int nframes, int k, uint8_t *d_modes,
+                    int32_t *d_costs_k, void *stream) {
+  if (!d_costs || nframes < 1 || width <= 0 || height <= 0) return fail("bad top-k arguments");
+  if (k < 1 || k > mipgpu::kMaxBestK) return fail("k %d out of range 1..%d", k, mipgpu::kMaxBestK);
+  if (!d_modes && !d_costs_k) return 0;
+  const long long cus = (long long)nframes * mip_num_ctus(width, height) * MIP_CUS_PER_CTU;
+  if (cus > (1LL << 31) - 256) return fail("too many CUs");
+  mipgpu::BestArgs b{d_costs, d_modes, d_costs_k, (int)cus, k};
+  HIP_TRY(mipgpu::launch_best_modes(b, (hipStream_t)stream));
   return 0;
 }
 
@@ -504,7 +519,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     }
   }
   if (d_best || d_best_cost) {
-    mipgpu::BestArgs b{d_costs, d_best, d_best_cost, nframes * e->nctus * MIP_CUS_PER_CTU};
+    mipgpu::BestArgs b{d_costs, d_best, d_best_cost, nframes * e->nctus * MIP_CUS_PER_CTU, e->opts.best_k};
     HIP_TRY(mipgpu::launch_best_modes(b, s));
   }
   return 0;
@@ -528,7 +543,7 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
     HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
-  const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU;
+  const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
   // Chunks of `sb` frames alternate between the two halves of the engine buffers, each half
   // with its own stream (H2D, [filter], search, D2H in order), so the transfers of one chunk
   // overlap the search of the next.  Transfers run at DMA rate from page-locked host

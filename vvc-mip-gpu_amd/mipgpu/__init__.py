@@ -54,7 +54,7 @@ def filter_index(name) -> int:
 
 class _Opts(ctypes.Structure):
     _fields_ = [("filter", ctypes.c_int), ("kernel_idx", ctypes.c_int), ("max_batch", ctypes.c_int),
-                ("want_sad_satd", ctypes.c_int), ("slices_per_ctu", ctypes.c_int)]
+                ("want_sad_satd", ctypes.c_int), ("slices_per_ctu", ctypes.c_int), ("best_k", ctypes.c_int)]
 
 
 _lib = None
@@ -84,6 +84,7 @@ def library():
         "mip_search_frames": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp]),
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
+        "mip_topk_device": (ip, [vp, ip, ip, ip, ip, vp, vp, vp]),
         "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
         "mip_host_alloc": (ip, [ctypes.c_size_t, ctypes.POINTER(vp)]),
         "mip_host_free": (ip, [vp]),
@@ -127,7 +128,7 @@ class MipEngine:
     """One engine per GPU (mip_engine_create).  Not thread safe."""
 
     def __init__(self, width: int, height: int, device: int = 0, filter=None, kernel_idx: int = 0,
-                 max_batch: int = 1, want_sad_satd: bool = False, slices_per_ctu: int = 0):
+                 max_batch: int = 1, want_sad_satd: bool = False, slices_per_ctu: int = 0, best_k: int = 1):
         L = library()
         self.width, self.height = int(width), int(height)
         self.nctus = num_ctus(self.width, self.height)
@@ -135,7 +136,9 @@ class MipEngine:
         self.kernel_idx = int(kernel_idx)
         self.max_batch = int(max_batch)
         self.want_sad_satd = bool(want_sad_satd)
-        o = _Opts(self.filter, self.kernel_idx, self.max_batch, int(self.want_sad_satd), int(slices_per_ctu))
+        self.best_k = int(best_k)
+        o = _Opts(self.filter, self.kernel_idx, self.max_batch, int(self.want_sad_satd), int(slices_per_ctu),
+                  self.best_k)
         h = ctypes.c_void_p()
         _check(L.mip_engine_create(int(device), self.width, self.height, ctypes.byref(o), ctypes.byref(h)))
         self._h = h
@@ -177,8 +180,8 @@ class MipEngine:
 
     def search(self, frames, refs=None, costs=True, best=False, sad_satd=False, out=None):
         """Full MIP search of host frames ([F,H,W] or [H,W] uint16).  Returns a dict with
-        'cost' [F, nCTUs*97840] int32 and optionally 'best_mode' / 'best_cost' [F, nCTUs*5380],
-        'sad' / 'satd'.  `out` may supply any of these arrays (e.g. from pinned_empty, for
+        'cost' [F, nCTUs*97840] int32 and optionally 'best_mode' / 'best_cost' [F, nCTUs*5380]
+        (decision lists [F, nCTUs*5380, K] when the engine has best_k = K > 1), 'sad' / 'satd'.  `out` may supply any of these arrays (e.g. from pinned_empty, for
         DMA-rate transfers); the others are allocated."""
         f = self._frames(frames)
         r = None if refs is None else self._frames(refs)
@@ -188,17 +191,19 @@ class MipEngine:
         def buf(key, want, cols, dtype):
             if not want:
                 return None
+            shape = (n,) + (cols if isinstance(cols, tuple) else (cols,))
             a = given.get(key)
             if a is None:
-                return np.empty((n, cols), dtype)
-            if a.dtype != np.dtype(dtype) or a.shape != (n, cols) or not a.flags.c_contiguous:
-                raise MipError(f"out[{key!r}] must be a C-contiguous {np.dtype(dtype)} array of shape {(n, cols)}")
+                return np.empty(shape, dtype)
+            if a.dtype != np.dtype(dtype) or a.shape != shape or not a.flags.c_contiguous:
+                raise MipError(f"out[{key!r}] must be a C-contiguous {np.dtype(dtype)} array of shape {shape}")
             return a
 
         out = {}
         cost = buf("cost", costs, self.costs_per_frame, np.int32)
-        bm = buf("best_mode", best, self.cus_per_frame, np.uint8)
-        bc = buf("best_cost", best, self.cus_per_frame, np.int32)
+        bcols = self.cus_per_frame if self.best_k == 1 else (self.cus_per_frame, self.best_k)
+        bm = buf("best_mode", best, bcols, np.uint8)
+        bc = buf("best_cost", best, bcols, np.int32)
         sad = buf("sad", sad_satd, self.costs_per_frame, np.int32)
         satd = buf("satd", sad_satd, self.costs_per_frame, np.int32)
         _check(library().mip_search_frames(self._h, _ptr(f), _ptr(r), n, _ptr(cost), _ptr(bm), _ptr(bc),
@@ -238,6 +243,22 @@ class MipEngine:
         return ms
 
 
+def topk_device(costs, width, height, k, modes=None, costs_k=None, stream=None):
+    """Per-CU decision lists of device cost tables (torch int32 [F, nCTUs*97840]):
+    returns (modes uint8, costs int32), each [F, nCTUs*5380, k] (mip_topk_device)."""
+    import torch
+    n = costs.shape[0]
+    shape = (n, num_ctus(width, height) * CUS_PER_CTU, int(k))
+    if modes is None:
+        modes = torch.empty(shape, dtype=torch.uint8, device=costs.device)
+    if costs_k is None:
+        costs_k = torch.empty(shape, dtype=torch.int32, device=costs.device)
+    s = stream if stream is not None else torch.cuda.current_stream(costs.device)
+    _check(library().mip_topk_device(_ptr(costs), int(width), int(height), n, int(k), _ptr(modes), _ptr(costs_k),
+                                     ctypes.c_void_p(s.cuda_stream)))
+    return modes, costs_k
+
+
 def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
     import torch
     n, h, w = frames_in.shape
@@ -247,5 +268,6 @@ def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
     return frames_out
 
 
-__all__ = ["MipEngine", "MipError", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "library", "pinned_empty",
+__all__ = ["MipEngine", "MipError", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "topk_device", "library",
+           "pinned_empty",
            "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]

@@ -130,3 +130,45 @@ def best_modes(costs: np.ndarray, nctus: int):
         modes_out.append(am.astype(np.uint8))
         cost_out.append(mn.astype(np.int32))
     return np.concatenate(modes_out, axis=1).reshape(-1), np.concatenate(cost_out, axis=1).reshape(-1)
+
+
+def topk_modes(costs: np.ndarray, nctus: int, k: int):
+    """Per-CU decision lists (numpy statement of mip_topk_device): the k lowest-cost modes
+    in increasing cost order, ties to the lower mode; 0xff / UNAVAILABLE past the CU's
+    modes and for unavailable CUs.  Returns (modes uint8, costs int32), [nctus*5380, k]."""
+    costs = costs.reshape(nctus, COSTS_PER_CTU)
+    modes_out, cost_out = [], []
+    for s in SHAPES:
+        blk = costs[:, s.cost_offset:s.cost_offset + s.ncu * s.total_modes].reshape(nctus, s.ncu, s.total_modes)
+        order = np.argsort(blk, axis=2, kind="stable")[..., :k]
+        val = np.take_along_axis(blk, order, axis=2)
+        pad = k - order.shape[2]
+        if pad > 0:
+            order = np.concatenate([order, np.full(order.shape[:2] + (pad,), 0xFF)], axis=2)
+            val = np.concatenate([val, np.full(val.shape[:2] + (pad,), UNAVAILABLE)], axis=2)
+        dead = blk[..., :1] == UNAVAILABLE
+        order = np.where(dead, 0xFF, order)
+        val = np.where(dead, UNAVAILABLE, val)
+        modes_out.append(order.astype(np.uint8))
+        cost_out.append(val.astype(np.int32))
+    return (np.concatenate(modes_out, axis=1).reshape(-1, k), np.concatenate(cost_out, axis=1).reshape(-1, k))
+
+
+BINARY_LOG_MAGIC = 0x4350494D  # "MIPC"
+
+
+def read_binary_log(path: str):
+    """Read a CLI --BinaryLog file: dict with width, height, frames and 'cost' (and 'sad',
+    'satd' when logged) as int32 [frames, nCTUs*97840] arrays (memory-mapped)."""
+    hdr = np.fromfile(path, dtype="<u4", count=8)
+    if hdr.size != 8 or hdr[0] != BINARY_LOG_MAGIC or hdr[1] != 1:
+        raise ValueError(f"{path}: not a version-1 MIP cost log")
+    w, h, n, per, flags = (int(v) for v in hdr[2:7])
+    if per != num_ctus(w, h) * COSTS_PER_CTU:
+        raise ValueError(f"{path}: {per} entries per frame do not match {w}x{h}")
+    names = ["cost"] + (["sad", "satd"] if flags & 1 else [])
+    mm = np.memmap(path, dtype="<i4", mode="r", offset=32, shape=(len(names), n, per))
+    out = {"width": w, "height": h, "frames": n}
+    for i, k in enumerate(names):
+        out[k] = mm[i]
+    return out
