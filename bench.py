@@ -298,11 +298,24 @@ def main():
             pinned_fps = 3 * B / (time.perf_counter() - t0)
             t0 = time.perf_counter()
             eng.search(host)
+            pageable_fps = B / (time.perf_counter() - t0)
+            # decisions only: frames in, per-CU best mode + cost out (the cost tables stay in HBM)
+            dout = {"best_mode": pinned_empty((B, eng.cus_per_frame), np.uint8),
+                    "best_cost": pinned_empty((B, eng.cus_per_frame), np.int32)}
+            eng.search(hp, costs=False, best=True, out=dout)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                eng.search(hp, costs=False, best=True, out=dout)
+            decisions_fps = 3 * B / (time.perf_counter() - t0)
             res["end_to_end"] = {"value": round(pinned_fps, 2), "unit": "frames/s",
-                                 "pageable_value": round(B / (time.perf_counter() - t0), 2),
+                                 "pageable_value": round(pageable_fps, 2),
+                                 "decisions_value": round(decisions_fps, 2),
                                  "note": "host frames in, host int32 cost tables out (H2D + search + D2H, "
-                                         "%.1f MB per frame over PCIe); value: page-locked buffers" %
-                                         (algorithmic_bytes_per_frame(W, H) / 1e6)}
+                                         "%.1f MB per frame over PCIe); value: page-locked buffers; "
+                                         "decisions_value: page-locked frames in, per-CU best mode + cost out "
+                                         "(%.1f MB per frame)" %
+                                         (algorithmic_bytes_per_frame(W, H) / 1e6,
+                                          (2 * W * H + 5 * eng.cus_per_frame) / 1e6)}
         if world == 1 and not args.no_reference_gpu:
             ref = reference_gpu(W, H, min(B, 4), args.seed)
             if ref is not None:

@@ -62,13 +62,15 @@ def test_full_size_configs_vs_reference(gpu_available, name):
             assert G.sha(filt[f]) == fr["filtered_sha256"]
 
 
+@pytest.mark.parametrize("w,h", [(392, 136), (648, 232)])
 @pytest.mark.parametrize("filt,nk", FILTERS)
-def test_filters_vs_oracle(gpu_available, filt, nk):
-    frame = synth_frame(392, 136, 0x51, 1)  # partial tiles on both axes
+def test_filters_vs_oracle(gpu_available, filt, nk, w, h):
+    # partial tiles on both axes; 648x232 has 6 interior tiles (vectorised staging path)
+    frame = synth_frame(w, h, 0x51, 1)
     # near-black samples: quotients around 1/2 (sum == scale/2 is the case where the
     # reference's fp32 division can fall just below the tie)
-    dark = np.random.default_rng(5).integers(0, 3, (136, 392)).astype(np.uint16)
-    with MipEngine(392, 136) as eng:
+    dark = np.random.default_rng(5).integers(0, 3, (h, w)).astype(np.uint16)
+    with MipEngine(w, h) as eng:
         for k in range(nk):
             for fr in (frame, dark):
                 got = eng.filter_frames(fr, filt, k)[0]

@@ -120,6 +120,19 @@ __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, i
   constexpr int TW = 128 + 2 * RAD;
   const int t = threadIdx.x;
   bool invalid = false;
+  // Interior tile: with a margin of one tile / 16 samples to every frame border, every
+  // gate of every filter (tap_valid / sep_fetch / inner_value) admits every cell, so the
+  // tile and its halo are plain samples: rows -RAD..31+RAD, columns -8..135 as 16-byte
+  // loads (the LDS row pitch is exactly those 144 columns).
+  if ((W & 7) == 0 && qx >= 128 && qy >= 32 && qx + 144 <= W - 2 && qy + 40 <= H - 2) {
+    constexpr int NV = (32 + 2 * RAD) * (kTWP / 8);
+    for (int i = t; i < NV; i += kThreads) {
+      const int r = i / (kTWP / 8), k = i - r * (kTWP / 8);
+      *reinterpret_cast<uint4 *>(tile + r * kTWP + 8 * k) =
+          *reinterpret_cast<const uint4 *>(in + (size_t)(qy - RAD + r) * W + qx - 8 + 8 * k);
+    }
+    return false;
+  }
   if ((W & 7) == 0) {
 #pragma unroll
     for (int p = 0; p < 4; p++) {
