@@ -1,11 +1,17 @@
 set -e
 cd /root/repo
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1 || { tail -30 gpurun_out/pt.log; exit 1; }
-tail -2 gpurun_out/pt.log
-for lib in filt0 filt1; do MIPGPU_LIB=$PWD/abtest/$lib.so timeout -k 10 120 python tools/filter_bench.py > gpurun_out/fb_$lib.json 2>/dev/null; done
+export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 -L > gpurun_out/avail.txt 2>&1 || true
+grep -i "icache\|SQC_" gpurun_out/avail.txt | head -40
+timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE -d gpurun_out/ic -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter --no-end-to-end > gpurun_out/ic.log 2>&1 || { tail -5 gpurun_out/ic.log; exit 1; }
 python - <<'PY'
-import json
-for lib in ("filt0","filt1"):
-    d=json.load(open("gpurun_out/fb_%s.json"%lib))
-    print(lib, {k[12:]: v["ms_per_launch"] for k,v in d["filters"].items()}, d.get("copy_calibration"))
+import csv,glob,collections
+per=collections.defaultdict(float)
+for p in glob.glob("gpurun_out/ic/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(p)):
+        if "mip_search" in r["Kernel_Name"]:
+            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+agg=collections.defaultdict(list)
+for (d,c),v in per.items(): agg[c].append(v)
+print({c: sum(v)/len(v) for c,v in agg.items()})
 PY
