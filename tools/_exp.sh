@@ -1,17 +1,7 @@
 set -e
 cd /root/repo
-export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 -L > gpurun_out/avail.txt 2>&1 || true
-grep -i "icache\|SQC_" gpurun_out/avail.txt | head -40
-timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE -d gpurun_out/ic -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter --no-end-to-end > gpurun_out/ic.log 2>&1 || { tail -5 gpurun_out/ic.log; exit 1; }
-python - <<'PY'
-import csv,glob,collections
-per=collections.defaultdict(float)
-for p in glob.glob("gpurun_out/ic/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(p)):
-        if "mip_search" in r["Kernel_Name"]:
-            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-agg=collections.defaultdict(list)
-for (d,c),v in per.items(): agg[c].append(v)
-print({c: sum(v)/len(v) for c,v in agg.items()})
-PY
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1 || { tail -30 gpurun_out/pt.log; exit 1; }
+tail -2 gpurun_out/pt.log
+b() { MIPGPU_LIB=$PWD/abtest/$1.so timeout -k 10 120 python bench.py $2 --steps 20 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter --no-end-to-end 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1 $2', d['value'], d['roofline']['kernel_ms_per_launch'])"; }
+for r in 1 2; do for lib in novar var; do b $lib ""; done; done
+for lib in novar var; do b $lib "--width 3840 --height 2160 --frames-per-step 8"; done

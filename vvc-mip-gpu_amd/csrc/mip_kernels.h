@@ -24,22 +24,25 @@ struct WaveTask {
   uint32_t cu0;   // first CU in the job array
 };
 
-constexpr int kNumClasses = 17;
-constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 16, 4, 8, 8, 4, 4};
-constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4};
-constexpr int size_class(int w, int h) {
-  for (int i = 0; i < kNumClasses; i++)
+// Size classes: W x H with V row parts per CU.  Classes 0-16 are the base class of each CU
+// size (row parts: classes with few CUs per quadrant split each CU's rows over V lanes per
+// strip so that a task still fills the wave); 17-19 are variants with more row parts, used
+// for the remainder group of a class whose CU count per quadrant is not a multiple of its
+// task size (e.g. 28 CUs of 32x8 = 3 tasks of 8 + one task of 4 CUs with V = 2).
+constexpr int kNumClasses = 20;
+constexpr int kNumBaseClasses = 17;
+constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 16, 4, 8, 8, 4, 4, 32, 16, 16};
+constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4, 8, 16, 8};
+constexpr int kClassV[kNumClasses] = {4, 2, 2, 4, 1, 1, 2, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2};
+constexpr int kClassVariant[kNumClasses] = {-1, -1, -1, -1, 17, -1, 18, 19, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                            -1, -1, -1};  // remainder-task class of a base class
+constexpr int size_class(int w, int h) {  // base class of a CU size
+  for (int i = 0; i < kNumBaseClasses; i++)
     if (kClassW[i] == w && kClassH[i] == h) return i;
   return -1;
 }
 constexpr int class_size_id(int w, int h) { return (w == 4 && h == 4) ? 0 : ((w == 4 || h == 4 || (w == 8 && h == 8)) ? 1 : 2); }
-// Row parts: classes with few CUs per quadrant split each CU's rows over V lanes per strip
-// so that a task still fills the wave.
-constexpr int class_row_parts(int w, int h) {
-  return (w == 64 || (w == 16 && h >= 32)) ? 4
-         : ((w == 32 && h >= 16) || (w == 4 && h >= 16) || (w == 16 && h == 16)) ? 2 : 1;
-}
-constexpr int class_slots(int w, int h) { return 64 / ((w / 4) * class_row_parts(w, h)); }
+constexpr int class_slots(int cls) { return 64 / ((kClassW[cls] / 4) * kClassV[cls]); }
 
 struct SearchArgs {
   const uint16_t *orig;   // [frames][height][width] original samples (distortion)

@@ -119,8 +119,8 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Compile-time geometry of a size class (W x H).
-template <int W, int H>
+// Compile-time geometry of a size class (W x H, VP row parts; default: the base class).
+template <int W, int H, int VP = kClassV[size_class(W, H)]>
 struct Geo {
   static constexpr int SID = class_size_id(W, H);
   static constexpr int R = SID == 2 ? 8 : 4;          // reduced prediction side
@@ -129,8 +129,8 @@ struct Geo {
   static constexpr int UH = W / R, UV = H / R;        // upsampling factors
   static constexpr int LH = ilog2c(UH), LV = ilog2c(UV);
   static constexpr int S = W / 4;                     // column strips per CU
-  static constexpr int V = class_row_parts(W, H);     // row parts per CU
-  static constexpr int SLOTS = class_slots(W, H);     // CUs per task
+  static constexpr int V = VP;                        // row parts per CU
+  static constexpr int SLOTS = 64 / (S * V);          // CUs per task
   static constexpr int KV = R / V;                    // upsampling windows per row part
   static constexpr bool CHUNKED = SID == 2 && UH == 1;  // 8xH: reduced rows in two halves
   static constexpr int CPOS = CHUNKED ? 32 : NOUT;    // scratch positions per chunk
@@ -392,10 +392,10 @@ struct OrigRows {
 // Walk one strip of one CU for one mode pair over upsampling windows [k0, k1) (rows for
 // UV == 1 and 4x4): prediction rows (upsampling, intra.cl:815-912) streamed through the
 // block transform.  `prev` is the anchor row above window k0 (vertical pass state).
-template <int W, int H, bool LAT, class RED>
+template <int W, int H, int V, bool LAT, class RED>
 __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &rt, const OrigRows<H> &orig,
                                            const RED &red, int x0, int k0, int k1, s2 (&prev)[4], Acc &acc) {
-  using G = Geo<W, H>;
+  using G = Geo<W, H, V>;
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
     BlockAcc b;
@@ -513,9 +513,9 @@ __device__ __forceinline__ uint32_t floor_sat(float f) { return (uint32_t)f; }
 // clip to packed pairs on read.  Results go to scratch[pos][slot] (16-bit
 // halves = modes), pos = stored position (transposed modes store output j at (j%R, j/R),
 // intra.cl:402-406, 485).  CHUNKED classes produce reduced rows [4*chunk, 4*chunk + 4).
-template <int W, int H, bool TR>
+template <int W, int H, int V, bool TR>
 __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, int chunk) {
-  using G = Geo<W, H>;
+  using G = Geo<W, H, V>;
   const int r = lane & 15, h = lane >> 4;
   const int m0 = TR ? 2 * q - G::MODES : 2 * q;
   // A: coefficient row of mode m0 + (h >> 1), inputs 4*(h & 1)..+3
@@ -577,10 +577,10 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   }
 }
 
-template <int W, int H>
+template <int W, int H, int V>
 __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, int chunk) {
-  if (q >= Geo<W, H>::MODES / 2) phase_a<W, H, true>(x, lane, ncu, q, chunk);
-  else phase_a<W, H, false>(x, lane, ncu, q, chunk);
+  if (q >= Geo<W, H>::MODES / 2) phase_a<W, H, V, true>(x, lane, ncu, q, chunk);
+  else phase_a<W, H, V, false>(x, lane, ncu, q, chunk);
 }
 
 // Sum over aligned groups of N adjacent lanes, delivered to the last lane of each group:
@@ -603,9 +603,9 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
-template <int W, int H, bool LAT>
+template <int W, int H, int V, bool LAT>
 __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, const WaveTask &task, int lane_in) {
-  using G = Geo<W, H>;
+  using G = Geo<W, H, V>;
   const int lane = opaque(lane_in);
   const SearchArgs &a = *x.a;
   const int ncu = task.ncu;
@@ -653,24 +653,24 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
     s2 prev[4];
 #pragma unroll
     for (int cc = 0; cc < 4; cc++) prev[cc] = top[cc];
-    phase_a<W, H>(x, lane, ncu, q, 0);
+    phase_a<W, H, V>(x, lane, ncu, q, 0);
     wave_lds_sync();
     if constexpr (G::CHUNKED) {
-      walk_strip<W, H>(c, rt, orig, red, x0, 0, 4, prev, acc);
+      walk_strip<W, H, V>(c, rt, orig, red, x0, 0, 4, prev, acc);
       wave_lds_sync();
-      phase_a<W, H>(x, lane, ncu, q, 1);
+      phase_a<W, H, V>(x, lane, ncu, q, 1);
       wave_lds_sync();
       const Red<G::R, G::RP> red_hi{mine, -4};  // chunk 1 holds reduced rows 4..7
-      walk_strip<W, H>(c, rt, orig, red_hi, x0, 4, 8, prev, acc);  // prev carries anchor row 3
+      walk_strip<W, H, V>(c, rt, orig, red_hi, x0, 4, 8, prev, acc);  // prev carries anchor row 3
     } else if constexpr (G::SID == 0) {
-      walk_strip<W, H>(c, rt, orig, red, x0, 0, 4, prev, acc);
+      walk_strip<W, H, V>(c, rt, orig, red, x0, 0, 4, prev, acc);
     } else {
       // row part v: windows [v*KV, (v+1)*KV) (rows when UV == 1)
       const int k0 = G::V > 1 ? v * G::KV : 0;
       if constexpr (G::V > 1 && G::UV > 1) {
         if (k0 > 0) anchor_row<W, H>(red, k0 - 1, x0, prev);
       }
-      walk_strip<W, H>(c, rt, orig, red, x0, k0, k0 + G::KV, prev, acc);
+      walk_strip<W, H, V>(c, rt, orig, red, x0, k0, k0 + G::KV, prev, acc);
     }
     wave_lds_sync();  // the scratch is rewritten by the next pair
     // ---- combine strips and row parts of one CU (adjacent lanes) into its last lane
@@ -794,17 +794,19 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
         const uint64_t c0 = clk ? __builtin_readcyclecounter() : 0;
         const WaveTask task = a.tasks[tbase + t];
         switch (task.cls) {
-#define MIP_CASE(idx, W, H)                                 \
-  case idx:                                                 \
-    static_assert(size_class(W, H) == idx, "class table");  \
-    if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)        \
-      run_task<W, H, ALT>(x, rt, task, lane);               \
+#define MIP_CASE(idx, W, H)                                                \
+  case idx:                                                                \
+    static_assert(kClassW[idx] == W && kClassH[idx] == H, "class table");  \
+    if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)                       \
+      run_task<W, H, kClassV[idx], ALT>(x, rt, task, lane);                \
     break;
           MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
           MIP_CASE(4, 32, 8) MIP_CASE(5, 8, 32) MIP_CASE(6, 16, 16) MIP_CASE(7, 16, 8)
           MIP_CASE(8, 8, 16) MIP_CASE(9, 32, 4) MIP_CASE(10, 4, 32) MIP_CASE(11, 16, 4)
           MIP_CASE(12, 4, 16) MIP_CASE(13, 8, 8) MIP_CASE(14, 8, 4) MIP_CASE(15, 4, 8)
           MIP_CASE(16, 4, 4)
+          // row-part variants for remainder tasks (mip_kernels.h)
+          MIP_CASE(17, 32, 8) MIP_CASE(18, 16, 16) MIP_CASE(19, 16, 8)
 #undef MIP_CASE
           default: break;
         }

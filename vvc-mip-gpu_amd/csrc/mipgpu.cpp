@@ -142,7 +142,7 @@ bool no_pairs() {
 // Estimated VALU instructions per lane for one mode pair of a task of `ncu` CUs.
 double pair_cost(int cls, int ncu) {
   const int w = mipgpu::kClassW[cls], h = mipgpu::kClassH[cls];
-  const int sid = mipgpu::class_size_id(w, h), v = mipgpu::class_row_parts(w, h);
+  const int sid = mipgpu::class_size_id(w, h), v = mipgpu::kClassV[cls];
   const int nout = sid == 2 ? 64 : 16;
   const double blocks = (double)h / 4 / v;
   const double mfma = ((ncu + 7) / 8) * (nout / 16);
@@ -177,20 +177,34 @@ WorkLists build_work(int slices, int waves, int width, int height) {
       }
     }
     double total = 0;
-    for (int cls = 0; cls < mipgpu::kNumClasses; cls++) {
+    for (int cls = 0; cls < mipgpu::kNumBaseClasses; cls++) {
       const std::vector<mipgpu::Job> &v = cls_cus[cls];
       if (v.empty()) continue;
-      const int slots = mipgpu::class_slots(mipgpu::kClassW[cls], mipgpu::kClassH[cls]);
-      const int ng = ((int)v.size() + slots - 1) / slots;
-      const int modes = mipgpu::class_size_id(mipgpu::kClassW[cls], mipgpu::kClassH[cls]) == 2 ? 6
-                        : (mipgpu::class_size_id(mipgpu::kClassW[cls], mipgpu::kClassH[cls]) == 1 ? 8 : 16);
-      for (int g = 0, at = 0; g < ng; g++) {  // equal-sized groups
-        const int n = ((int)v.size() - at) / (ng - g);
+      const int nv = (int)v.size(), slots = mipgpu::class_slots(cls);
+      const int sid = mipgpu::class_size_id(mipgpu::kClassW[cls], mipgpu::kClassH[cls]);
+      const int modes = sid == 2 ? 6 : (sid == 1 ? 8 : 16);
+      // groups (class, CUs): full tasks plus a remainder task of the class's row-part variant
+      // when the remainder fits it; otherwise equal-sized groups
+      std::vector<std::pair<int, int>> groups;
+      const int var = mipgpu::kClassVariant[cls], rem = nv % slots;
+      if (rem > 0 && var >= 0 && rem <= mipgpu::class_slots(var)) {
+        for (int g = 0; g < nv / slots; g++) groups.push_back({cls, slots});
+        groups.push_back({var, rem});
+      } else {
+        const int ng = (nv + slots - 1) / slots;
+        for (int g = 0, at = 0; g < ng; g++) {
+          const int n = (nv - at) / (ng - g);
+          groups.push_back({cls, n});
+          at += n;
+        }
+      }
+      for (int g = 0, at = 0; g < (int)groups.size(); g++) {
+        const int gc = groups[g].first, n = groups[g].second;
         const uint32_t first = (uint32_t)wl.jobs.size();
         wl.jobs.insert(wl.jobs.end(), v.begin() + at, v.begin() + at + n);
         at += n;
-        const double c = pair_cost(cls, n);
-        pieces.push_back({mipgpu::WaveTask{(uint8_t)cls, (uint8_t)n, 0, (uint8_t)modes, first}, c});
+        const double c = pair_cost(gc, n);
+        pieces.push_back({mipgpu::WaveTask{(uint8_t)gc, (uint8_t)n, 0, (uint8_t)modes, first}, c});
         total += c * modes;
       }
     }
