@@ -88,7 +88,8 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
                       int kernel_idx, uint16_t *out);
 
 /* Full MIP search of `nframes` host frames: H2D, [filter], search, D2H, in chunks of
- * max_batch/2 frames whose transfers overlap the next chunk's search (two streams).
+ * max_batch/4 (max_batch >= 16) or max_batch/2 frames over two streams, so that each
+ * chunk's transfers overlap the neighbouring chunks' searches.
  * Replaces the per-frame loop main.cpp:678-1241 + readMemobjsIntoArray_Distortion.
  * refs_or_null: caller-provided reference-sample frames (alternative samples computed
  * elsewhere); NULL = originals, or the engine's filter when opts.filter != NONE.

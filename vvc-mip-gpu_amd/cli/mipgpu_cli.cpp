@@ -77,7 +77,7 @@ void usage() {
                "  --AllFrames                       Log every frame (reference logs frame 0 only)\n"
                "  --BestModes arg                   Write the per-CU best mode / cost to this CSV\n"
                "  --BatchFrames arg (=8)            Frames per device batch\n"
-               "  --Threads arg (=0)                Log-formatting threads (0 = all cores)\n"
+               "  --Threads arg (=0)                CSV parsing / log-formatting threads (0 = all cores)\n"
                "  --TopK arg (=1)                   Modes per CU in the BestModes file (1..32, ranked)\n"
                "  --BinaryLog arg                   Write every frame's int32 cost table to this file\n"
                "  --InputFormat arg (=auto)         csv | u16 (raw 16-bit luma) | yuv420p10 (planar 4:2:0, 10 bit)\n";
@@ -199,28 +199,45 @@ struct Pinned {
   T &operator[](size_t i) { return p[i]; }
 };
 
-// Fast CSV reader (main.cpp:364-384 format).
-bool read_frames(const std::string &path, int W, int H, int n, uint16_t *out) {
+// CSV reader (main.cpp:364-384 format): the file is read whole, line starts are indexed,
+// and the H*n rows are parsed by `threads` threads.
+bool parse_row(const char *p, const char *end, int W, uint16_t *out) {
+  for (int x = 0; x < W; x++) {
+    while (p < end && (*p == ' ' || *p == '\r')) p++;
+    int v = 0;
+    bool any = false;
+    while (p < end && *p >= '0' && *p <= '9') v = v * 10 + (*p++ - '0'), any = true;
+    if (!any) return false;
+    out[x] = (uint16_t)v;
+    while (p < end && *p != ',' && *p != '\n') p++;
+    if (p < end && *p == ',') p++;
+  }
+  return true;
+}
+
+bool read_frames(const std::string &path, int W, int H, int n, uint16_t *out, int threads) {
   std::ifstream f(path, std::ios::binary);
   if (!f) return false;
   std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  memset(out, 0, (size_t)W * H * n * sizeof(uint16_t));
-  const char *p = data.c_str(), *end = p + data.size();
-  for (size_t row = 0; row < (size_t)H * n; row++) {
-    for (int x = 0; x < W; x++) {
-      while (p < end && (*p == ' ' || *p == '\r')) p++;
-      int v = 0;
-      bool any = false;
-      while (p < end && *p >= '0' && *p <= '9') v = v * 10 + (*p++ - '0'), any = true;
-      if (!any) return false;
-      out[row * W + x] = (uint16_t)v;
-      while (p < end && *p != ',' && *p != '\n') p++;
-      if (p < end && *p == ',') p++;
-    }
-    while (p < end && *p != '\n') p++;
-    if (p < end) p++;
+  const size_t rows = (size_t)H * n;
+  std::vector<size_t> start;
+  start.reserve(rows + 1);
+  for (size_t pos = 0; start.size() < rows && pos < data.size();) {
+    start.push_back(pos);
+    const void *nl = memchr(data.data() + pos, '\n', data.size() - pos);
+    pos = nl ? (size_t)((const char *)nl - data.data()) + 1 : data.size();
   }
-  return true;
+  if (start.size() < rows) return false;
+  start.push_back(data.size());
+  std::vector<char> ok(std::max(1, threads), 1);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < (int)ok.size(); t++)
+    pool.emplace_back([&, t] {
+      for (size_t r = t; r < rows; r += ok.size())
+        if (!parse_row(data.data() + start[r], data.data() + start[r + 1], W, out + r * W)) ok[t] = 0;
+    });
+  for (auto &th : pool) th.join();
+  return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
 }
 
 // Raw frames: `luma_only` = consecutive W x H little-endian 16-bit frames; otherwise planar
@@ -341,7 +358,8 @@ int main(int argc, char **argv) {
     return 1;
   }
   const std::string fmt = input_format(o);
-  const bool read_ok = fmt == "csv" ? read_frames(o.input, W, H, o.frames, frames.data())
+  const int threads = o.threads > 0 ? o.threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  const bool read_ok = fmt == "csv" ? read_frames(o.input, W, H, o.frames, frames.data(), threads)
                                     : read_raw_frames(o.input, W, H, o.frames, fmt == "u16", frames.data());
   if (!read_ok) {
     perror("error while opening samples files");
@@ -421,7 +439,6 @@ int main(int argc, char **argv) {
     sh.y.resize(sh.ncu);
     for (int cu = 0; cu < sh.ncu; cu++) mip_cu_position(s, cu, &sh.x[cu], &sh.y[cu]);
   }
-  const int threads = o.threads > 0 ? o.threads : (int)std::max(1u, std::thread::hardware_concurrency());
   // reportDistortionToFile=1 in the reference even when -l is not given (writes ".csv").
   {
     FILE *fp = fopen((o.prefix + ".csv").c_str(), "w");

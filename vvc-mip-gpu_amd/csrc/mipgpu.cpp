@@ -558,16 +558,20 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
     HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
   const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
-  // Chunks of `sb` frames alternate between the two halves of the engine buffers, each half
-  // with its own stream (H2D, [filter], search, D2H in order), so the transfers of one chunk
-  // overlap the search of the next.  Transfers run at DMA rate from page-locked host
-  // memory (mip_host_alloc); pageable buffers are staged by the runtime.
-  const int sb = e->opts.max_batch >= 2 ? e->opts.max_batch / 2 : 1;
+  // Chunks of `sb` frames rotate over `nslots` slots of the engine buffers (a quarter or a
+  // half of max_batch each) and alternate between two streams (H2D, [filter], search, D2H
+  // in order on each), so one chunk's transfers overlap the neighbouring chunks' searches
+  // and H2D / D2H run on both copy engines at once.  A slot is reused nslots chunks later,
+  // on the same stream (nslots is even), so stream order protects it.  Transfers run at DMA
+  // rate from page-locked host memory (mip_host_alloc); pageable buffers are staged by the
+  // runtime.
+  const int nslots = e->opts.max_batch >= 16 ? 4 : (e->opts.max_batch >= 2 ? 2 : 1);
+  const int sb = e->opts.max_batch / nslots;
   for (int f0 = 0, k = 0; f0 < nframes; f0 += sb, k++) {
     const int nb = std::min(sb, nframes - f0);
-    const int h = e->opts.max_batch >= 2 ? (k & 1) : 0;
+    const int h = nslots > 1 ? (k & 1) : 0;
     const hipStream_t st = h ? e->stream2 : e->stream;
-    const size_t fo = (size_t)h * sb;  // first engine frame slot of this half
+    const size_t fo = (size_t)(k % nslots) * sb;  // first engine frame slot of this chunk
     uint16_t *d_frames = e->d_frames + fo * fs;
     HIP_TRY(hipMemcpyAsync(d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, st));
     const uint16_t *d_refs = nullptr;
