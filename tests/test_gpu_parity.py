@@ -166,6 +166,29 @@ def test_topk_decision_lists(gpu_available, k):
         assert np.array_equal(modes[0, :, 0].cpu().numpy(), bm)
 
 
+def test_full_size_ctu_shift_and_batch_invariance(gpu_available):
+    """Size-independent properties at the bench's 1080p size: (a) shifting a frame right by
+    one CTU (128 columns) shifts every CTU's cost block by one CTU, except CTUs whose left
+    reference column changes (first column); (b) a frame's table does not depend on the
+    batch it is searched in (persistent item queue, edge-CTU lists, slice choice)."""
+    W, H = 1920, 1080
+    a = synth_frame(W, H, 0xB1, 0)
+    b = np.empty_like(a)
+    b[:, 128:] = a[:, :W - 128]
+    b[:, :128] = synth_frame(128, H, 0xB2, 1)
+    cols, rows = layout.ctu_grid(W, H)
+    batch = np.stack([a, b, synth_frame(W, H, 0xB3, 0)])
+    with MipEngine(W, H, max_batch=3) as eng:
+        ca = eng.search(a)["cost"][0].reshape(-1, layout.COSTS_PER_CTU)
+        cb = eng.search(b)["cost"][0].reshape(-1, layout.COSTS_PER_CTU)
+        cbatch = eng.search(batch)["cost"]
+    for r in range(rows):
+        for c in range(1, cols - 1):
+            assert np.array_equal(ca[r * cols + c], cb[r * cols + c + 1]), (r, c)
+    assert np.array_equal(cbatch[0].reshape(ca.shape), ca)
+    assert np.array_equal(cbatch[1].reshape(cb.shape), cb)
+
+
 def test_errors_are_loud(gpu_available):
     with pytest.raises(MipError):
         MipEngine(130, 64)  # width not a multiple of 4

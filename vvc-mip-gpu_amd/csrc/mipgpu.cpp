@@ -280,12 +280,12 @@ struct mip_engine {
 };
 
 namespace {
-// Slice count for a launch of `nframes`: ~4 quadrant workgroups per CU slot or more
-// (measured on MI355X at 1080p: 1 frame -> 4 slices 4246 vs 3444 frames/s, 2-4 frames -> 2,
-// >= 8 frames -> 1).
+// Slice count for a launch of `nframes`: items (quadrant x slice) for the persistent grid of
+// 512 workgroups.  Measured on MI355X at 1080p: 1 frame -> 2 slices 5076 frames/s (1: 4842,
+// 4: 4770), >= 2 frames -> 1 slice (2 frames: 5830 vs 5087 with 2 slices).
 const mip_engine::Work &pick_work(const mip_engine *e, int nframes) {
   const long long wg1 = 4LL * e->nctus * nframes;  // workgroups at one slice
-  const int want = wg1 < 1000 ? 4 : (wg1 < 4500 ? 2 : 1);
+  const int want = wg1 < 1000 ? 2 : 1;
   const mip_engine::Work *best = &e->work[0];
   for (const mip_engine::Work &w : e->work)
     if (std::abs(w.slices - want) < std::abs(best->slices - want)) best = &w;
