@@ -7,9 +7,12 @@
 // ~1.2 GB of reduced predictions per 1080p frame, main.cpp:443-444).
 //
 // Work decomposition
-//   workgroup = (CTU quadrant, slice), 8 waves.  No CU of the 47 shapes straddles a 64x64
-//               quadrant, so a workgroup stages only its quadrant (+1 row above, +4 columns
-//               left: the reference samples) and the MIP matrices in LDS.
+//   workgroup = persistent, 8 waves; takes items = (frame, CTU, quadrant, slice) from a
+//               device-wide counter.  No CU of the 47 shapes straddles a 64x64 quadrant, so
+//               an item stages only its quadrant (+1 row above, +4 columns left: the
+//               reference samples) in LDS; the MIP matrices are staged once per workgroup.
+//               CTUs cut by the frame border have their own lists (CUs outside the frame
+//               get MIP_COST_UNAVAILABLE and no work).
 //   wave      = a list of tasks (host-built, load balanced).  A task is up to 64/(S*V) CUs
 //               of ONE size class W x H (S = W/4 column strips, V = row parts) and a range
 //               of mode pairs; every loop bound is a compile-time constant of the class.
