@@ -41,6 +41,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "1080p frames/sec, full MIP mode search over all CU sizes; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E peak (spec)
+MFMA_F16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md, dense f16/bf16 matrix peak
 # VALU issue: 256 CUs x 4 SIMDs, one wave64 instruction per 4 cycles each, 2.4 GHz
 # (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s.
 VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
@@ -98,6 +99,15 @@ def valu_section(pmc, kernel_ms, alg_ops):
     if insts:
         rate = insts / (kernel_ms * 1e-3)
         out["achieved"], out["frac"] = round(rate / 1e9, 1), round(rate / VALU_PEAK_INSTS, 4)
+    flops = pmc.get("mfma_f16_flops_per_launch")
+    if flops:
+        # phase A (the MIP matrix products) on the matrix cores: f16 MFMA rate vs the dense peak
+        tf = flops / (kernel_ms * 1e-3) / 1e12
+        out["mfma"] = {"unit": "TFLOP/s", "achieved": round(tf, 2), "peak": MFMA_F16_PEAK_TFLOPS,
+                       "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 5),
+                       "insts_per_launch": pmc.get("mfma_insts_per_launch"),
+                       "busy_utilization": pmc.get("mfma_busy_utilization"),
+                       "note": "block-diagonal K: half of each 16x16x16 product multiplies zeros"}
     return out
 
 

@@ -12,7 +12,8 @@ import os
 import sys
 
 root, key, out = sys.argv[1], sys.argv[2], sys.argv[3]
-COUNTERS = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE")
+COUNTERS = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+            "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16")
 SEARCH = "mip_search_kernel<false>"          # original-reference search (the bench `value`)
 FILTER = "filter_kernel<2, true, false>"    # BASELINE configs[2] filter (bench `filter`)
 
@@ -56,6 +57,13 @@ rec.update({"kernel": SEARCH, "valu_insts_per_launch": valu, "gui_active_cycles_
             "lds_bank_conflict_frac": conf and lds and round(conf / lds, 4),
             "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/pmc_profile.sh); "
                       "FETCH_SIZE KiB x1024 x2 (gfx950 correction), WRITE_SIZE KiB x1024"})
+# Matrix cores (phase A of the search): MFMA instructions, busy cycles summed over the
+# 1024 SIMDs, and f16 MOPs (x512 = flops, as rocprofv3's MfmaFlopsF16 derives them).
+mfma, busy, mops = mean(s_vals, "SQ_INSTS_MFMA"), mean(s_vals, "SQ_VALU_MFMA_BUSY_CYCLES"), \
+    mean(s_vals, "SQ_INSTS_VALU_MFMA_MOPS_F16")
+if mfma is not None:
+    rec.update({"mfma_insts_per_launch": mfma, "mfma_f16_flops_per_launch": mops and mops * 512,
+                "mfma_busy_utilization": busy and grbm and round(busy / (1024 * grbm / 8), 4)})
 f = traffic(collect(FILTER))
 if f:
     f["kernel"] = FILTER
