@@ -252,3 +252,56 @@ def test_8k_alt_int_sampled_ctus(gpu_available):
         oc = O.search(frame, refs, ctus=(c, c + 1))
         sl = slice(c * layout.COSTS_PER_CTU, (c + 1) * layout.COSTS_PER_CTU)
         assert np.array_equal(cost[sl], oc[sl]), c
+
+
+@pytest.mark.parametrize("filt,k", [(None, 0), ("filterFrame_2d_float_5x5_quarterCtu", 2)])
+def test_host_pipeline_four_slots_uneven_chunks(gpu_available, filt, k):
+    """mip_search_frames with max_batch >= 16: 4 engine buffer slots over 2 streams, chunks
+    of max_batch/4 frames, an uneven last chunk (19 frames = 4+4+4+4+3), all outputs.
+    Every frame must equal the device API on the same frames and the oracle."""
+    import torch
+    w, h, n = 264, 136, 19
+    frames = synth_frames(w, h, n, 0x4F0, 0)
+    with MipEngine(w, h, max_batch=16, filter=filt, kernel_idx=k, want_sad_satd=True) as eng:
+        host = eng.search(frames, best=True, sad_satd=True)
+        d = torch.from_numpy(frames.astype(np.int16)).cuda()
+        dev = np.concatenate([eng.search_device(d[:16]).cpu().numpy(), eng.search_device(d[16:]).cpu().numpy()])
+    assert np.array_equal(host["cost"], dev)
+    nct = layout.num_ctus(w, h)
+    for f in range(n):
+        refs = O.filter_frame(frames[f], filt, k) if filt else None
+        oc, osad, osatd = O.search(frames[f], refs, want_sad_satd=True)
+        assert np.array_equal(host["cost"][f], oc), f
+        assert np.array_equal(host["sad"][f], osad), f
+        assert np.array_equal(host["satd"][f], osatd), f
+        bm, bc = layout.best_modes(oc, nct)
+        assert np.array_equal(host["best_mode"][f], bm), f
+        assert np.array_equal(host["best_cost"][f], bc), f
+
+
+def test_engine_filter_scratch_shared_by_two_streams(gpu_available):
+    """Device-API searches that filter into the engine's reference scratch (no caller
+    references) on two streams, with different frames per launch: each launch must wait
+    for the previous reader of the scratch (refs_done), so every table matches the oracle;
+    a host-API call in between must wait as well."""
+    import torch
+    filt, k = "filterFrame_2d_float_5x5_quarterCtu", 2
+    w, h = 264, 200
+    frames = synth_frames(w, h, 4, 0x5C, 0)
+    want = np.stack([O.search(frames[f], O.filter_frame(frames[f], filt, k)) for f in range(4)])
+    d = torch.from_numpy(frames.astype(np.int16)).cuda()
+    pairs = [d[[f0, (f0 + 1) % 4]].contiguous() for f0 in range(4)]
+    torch.cuda.synchronize()  # the gathers ran on the current stream
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    with MipEngine(w, h, max_batch=2, filter=filt, kernel_idx=k) as eng:
+        outs = []
+        for i in range(24):
+            f0 = (i * 3) % 4
+            sel = [f0, (f0 + 1) % 4]
+            outs.append((sel, eng.search_device(pairs[f0], stream=streams[i % 2])))
+            if i == 11:
+                mid = eng.search(frames[2:4])["cost"]
+        torch.cuda.synchronize()
+        for sel, c in outs:
+            assert np.array_equal(c.cpu().numpy(), want[sel])
+        assert np.array_equal(mid, want[2:4])

@@ -109,7 +109,10 @@ struct FilterArgs {
 };
 
 int search_waves_per_group();
-hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, hipStream_t s);
+// Workgroups of the search kernel resident on the current device at once (persistent grid
+// size); computed once per engine (mip_engine_create), 0 on error.
+int search_resident_groups(bool alt_refs);
+hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, hipStream_t s);
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s);
 

@@ -881,31 +881,21 @@ size_t search_lds_bytes(bool alt) {
   return (size_t)(kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes + (size_t)kWaves * kWaveBytes + 16;
 }
 
-// Workgroups resident on the device at once (persistent grid size).
-static int resident_groups(bool alt) {
-  static int cached[2] = {0, 0};
-  int &n = cached[alt ? 1 : 0];
-  if (n == 0) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 0;
-    const hipError_t e = alt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<true>, 64 * kWaves,
-                                                                            search_lds_bytes(true))
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<false>, 64 * kWaves,
-                                                                            search_lds_bytes(false));
-    if (e != hipSuccess || per_cu < 1) return 0;
-    n = cus * per_cu;
-  }
-  return n;
+int search_resident_groups(bool alt) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const hipError_t e = alt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<true>, 64 * kWaves,
+                                                                          search_lds_bytes(true))
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<false>, 64 * kWaves,
+                                                                          search_lds_bytes(false));
+  return e == hipSuccess && per_cu >= 1 ? cus * per_cu : 0;
 }
 
-hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, hipStream_t s) {
-  if (args.slices < 1 || !args.queue) return hipErrorInvalidValue;
+hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, hipStream_t s) {
+  if (args.slices < 1 || !args.queue || resident < 1) return hipErrorInvalidValue;
   SearchArgs a = args;
   a.nitems = (uint32_t)(4 * a.slices) * a.nctus * nframes;
-  const int resident = resident_groups(alt_refs);
-  if (resident < 1) return hipErrorInvalidDevice;
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const size_t lds = search_lds_bytes(alt_refs);

@@ -269,6 +269,13 @@ struct mip_engine {
   };
   std::vector<Work> work;
   uint8_t *d_tables = nullptr;
+  int resident[2] = {0, 0};  // persistent search grid (workgroups resident on this device), [alt]
+  // Engine-owned reference scratch d_refs, written by the engine filter when a device-API
+  // search has no caller references: every such search records refs_done on its stream, and
+  // the next writer of d_refs (another device-API search, on any stream, or a host-API call)
+  // waits for it first.
+  hipEvent_t refs_done = nullptr;
+  bool refs_pending = false;
   // Item-counter pairs of the persistent search kernel, used round robin; a pair is reused
   // only after the launch that last used it has completed (stream wait on its event), so
   // launches on different streams never share one.
@@ -280,6 +287,9 @@ struct mip_engine {
 };
 
 namespace {
+// CU count limit of one launch (int32 indices in the decision-list kernel).
+constexpr long long kMaxCus = (1LL << 31) - 256;
+
 // Slice count for a launch of `nframes`: items (quadrant x slice) for the persistent grid of
 // 512 workgroups.  Measured on MI355X at 1080p: 1 frame -> 2 slices 5076 frames/s (1: 4842,
 // 4: 4770), >= 2 frames -> 1 slice (2 frames: 5830 vs 5087 with 2 slices).
@@ -292,6 +302,16 @@ const mip_engine::Work &pick_work(const mip_engine *e, int nframes) {
   return *best;
 }
 }  // namespace
+
+// Host-API calls (synchronous) overwrite engine scratch: order them after the device-API
+// searches still reading d_refs; once the call has synchronised both engine streams,
+// those searches are complete too.
+static int wait_refs_readers(mip_engine *e) {
+  if (!e->refs_pending) return 0;
+  HIP_TRY(hipStreamWaitEvent(e->stream, e->refs_done, 0));
+  HIP_TRY(hipStreamWaitEvent(e->stream2, e->refs_done, 0));
+  return 0;
+}
 
 extern "C" {
 
@@ -347,6 +367,7 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->d_queue) (void)hipFree(e->d_queue);
   for (hipEvent_t ev : e->queue_done)
     if (ev) (void)hipEventDestroy(ev);
+  if (e->refs_done) (void)hipEventDestroy(e->refs_done);
   for (const mip_engine::Work &w : e->work)
     for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin})
       if (p) (void)hipFree(p);
@@ -365,6 +386,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   mip_opts_default(&o);
   if (opts) o = *opts;
   if (o.max_batch < 1) return fail("max_batch must be >= 1");
+  if ((long long)o.max_batch * mip_num_ctus(width, height) * MIP_CUS_PER_CTU > kMaxCus)
+    return fail("max_batch %d x %d CTUs exceeds %lld CUs per launch", o.max_batch, mip_num_ctus(width, height), kMaxCus);
   if (o.best_k == 0) o.best_k = 1;
   if (o.best_k < 1 || o.best_k > mipgpu::kMaxBestK) return fail("best_k %d out of range 1..%d", o.best_k, mipgpu::kMaxBestK);
   if (o.filter != MIP_FILTER_NONE) {
@@ -406,6 +429,11 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     return cleanup(fail("hipMemset failed"));
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
+  if (hipEventCreateWithFlags(&e->refs_done, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail("hipEventCreate failed"));
+  for (int alt = 0; alt < 2; alt++)
+    if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0)) < 1)
+      return cleanup(fail("cannot size the persistent search grid on device %d", device));
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
   std::vector<int> slice_set;
   if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
@@ -446,7 +474,7 @@ int mip_topk_device(const int32_t *d_costs, int width, int height, int nframes, 
   if (k < 1 || k > mipgpu::kMaxBestK) return fail("k %d out of range 1..%d", k, mipgpu::kMaxBestK);
   if (!d_modes && !d_costs_k) return 0;
   const long long cus = (long long)nframes * mip_num_ctus(width, height) * MIP_CUS_PER_CTU;
-  if (cus > (1LL << 31) - 256) return fail("too many CUs");
+  if (cus > kMaxCus) return fail("too many CUs");
   mipgpu::BestArgs b{d_costs, d_modes, d_costs_k, (int)cus, k};
   HIP_TRY(mipgpu::launch_best_modes(b, (hipStream_t)stream));
   return 0;
@@ -465,9 +493,13 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
                               int32_t *d_best_cost, hipStream_t s) {
   if (!e || !d_frames || !d_costs || nframes < 1) return fail("bad search arguments");
+  const long long total_cus = (long long)nframes * e->nctus * MIP_CUS_PER_CTU;
+  if (total_cus > kMaxCus) return fail("%d frames x %d CTUs exceed %lld CUs per launch", nframes, e->nctus, kMaxCus);
   const uint16_t *refs = d_refs;
-  if (!refs && e->opts.filter != MIP_FILTER_NONE) {
+  const bool engine_refs = !refs && e->opts.filter != MIP_FILTER_NONE;
+  if (engine_refs) {
     if (nframes > e->opts.max_batch) return fail("nframes %d > max_batch %d", nframes, e->opts.max_batch);
+    if (e->refs_pending) HIP_TRY(hipStreamWaitEvent(s, e->refs_done, 0));  // last reader of d_refs
     if (mip_filter_device(d_frames, e->d_refs, e->width, e->height, nframes, e->opts.filter,
                           e->opts.kernel_idx, s) != 0)
       return -1;
@@ -520,9 +552,13 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const int slot = (int)(e->queue_seq++ % mip_engine::kQueueSlots);
   if (e->queue_used[slot]) HIP_TRY(hipStreamWaitEvent(s, e->queue_done[slot], 0));
   a.queue = e->d_queue + 2 * slot;
-  HIP_TRY(mipgpu::launch_search(a, nframes, alt, s));
+  HIP_TRY(mipgpu::launch_search(a, nframes, alt, e->resident[alt ? 1 : 0], s));
   HIP_TRY(hipEventRecord(e->queue_done[slot], s));
   e->queue_used[slot] = true;
+  if (engine_refs) {
+    HIP_TRY(hipEventRecord(e->refs_done, s));
+    e->refs_pending = true;
+  }
   if (timing) {
     HIP_TRY(hipMemcpyAsync(clocks.data(), a.wave_clock, clocks.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -533,7 +569,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     }
   }
   if (d_best || d_best_cost) {
-    mipgpu::BestArgs b{d_costs, d_best, d_best_cost, nframes * e->nctus * MIP_CUS_PER_CTU, e->opts.best_k};
+    mipgpu::BestArgs b{d_costs, d_best, d_best_cost, (int)total_cus, e->opts.best_k};
     HIP_TRY(mipgpu::launch_best_modes(b, s));
   }
   return 0;
@@ -557,6 +593,7 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
     HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
+  if (wait_refs_readers(e) != 0) return -1;
   const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
   // Chunks of `sb` frames rotate over `nslots` slots of the engine buffers (a quarter or a
   // half of max_batch each) and alternate between two streams (H2D, [filter], search, D2H
@@ -599,6 +636,7 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream2));
+  e->refs_pending = false;
   return 0;
 }
 
@@ -620,6 +658,7 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
   HIP_TRY(hipSetDevice(e->device));
   const size_t fs = (size_t)e->width * e->height;
   if (!e->d_refs) HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
+  if (wait_refs_readers(e) != 0) return -1;
   for (int f0 = 0; f0 < nframes; f0 += e->opts.max_batch) {
     const int nb = std::min(e->opts.max_batch, nframes - f0);
     HIP_TRY(hipMemcpyAsync(e->d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, e->stream));
@@ -628,6 +667,8 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
     HIP_TRY(hipMemcpyAsync(out + f0 * fs, e->d_refs, nb * fs * 2, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
   }
+  HIP_TRY(hipStreamSynchronize(e->stream2));
+  e->refs_pending = false;
   return 0;
 }
 
