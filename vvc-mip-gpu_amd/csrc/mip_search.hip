@@ -68,13 +68,30 @@ constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
 constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 16;    // > every uniform B offset + 8 B
 constexpr int kUnavailable = 0x7fffffff;
 
+// Biased residuals.  The Hadamard butterflies of the SATD run as plain 32-bit adds /
+// subtracts on both 16-bit halves at once (v_add_u32 / v_sub_u32 issue at twice the rate
+// of the packed v_pk_* ops on gfx950, tools/valu_rate.hip), which is exact only while no
+// half ever goes negative or past 65535.  So every value carries a bias: the original
+// samples are staged into LDS as o + kBiasD[y & 1][x & 3] (the 4x4 block position), so the
+// residual o - p arrives biased, and the biases propagate through the butterflies to
+//   row stage 1 (s):  >= 2046,  row stage 2 (t): >= 4092,  column stage (u): >= 8184
+// -- each exactly the magnitude bound of that stage (|d| <= 1023 doubles per stage) -- with
+// every biased value below 40920.  The last column butterfly is folded as
+// |a+b| + |a-b| = 2 max(|a|, |b|) on pairs that share a bias: u0/u2 of column k carry
+// kBiasP[k], u1/u3 carry kBiasQ (2 * bias < 65536, see block_finish).
+constexpr uint32_t kBiasD[2][4] = {{15345, 1023, 3069, 1023}, {7161, 1023, 3069, 1023}};  // [row & 1][col]
+constexpr uint32_t kBiasP[4] = {32736, 24552, 16368, 16368};
+constexpr uint32_t kBiasQ = 8184;
+constexpr uint32_t splat32(uint32_t v) { return v | v << 16; }
+// a staged dword holds columns (x, x+1), x even: the biases of a block row's column pair
+constexpr uint32_t bias_word(int y, int x) { return kBiasD[y & 1][x & 3] | kBiasD[y & 1][(x + 1) & 3] << 16; }
+
 __device__ __forceinline__ int tidx(int x, int y) { return (y + 1) * kPitch + x + kColOff; }
 __device__ __forceinline__ s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
 __device__ __forceinline__ u2 as_u2(s2 v) { return __builtin_bit_cast(u2, v); }
 __device__ __forceinline__ s2 as_s2(u2 v) { return __builtin_bit_cast(s2, v); }
 __device__ __forceinline__ s2 splat(int v) { return s2{(short)v, (short)v}; }
 __device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
-__device__ __forceinline__ s2 smin(s2 a, s2 b) { return __builtin_elementwise_min(a, b); }
 
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
 
@@ -154,18 +171,22 @@ struct Geo {
 
 // ---- reference samples -------------------------------------------------------------
 // Full quadrant tile (original references): any (x, y) of rows -1..63, columns -4..63.
-// Lattice (ALT): rows y = 4i-1 and columns x = 4i-1 only -- all a CU boundary reads.
+// Its samples carry the residual bias (kBiasD), removed here: reference rows lie at
+// y = 4i - 1 (bias row 1) and reference columns at x = 4i - 1 (bias column 3 = 1023).
+// Lattice (ALT): rows y = 4i-1 and columns x = 4i-1 only -- all a CU boundary reads; unbiased.
 template <bool LAT>
 struct RefTile {
   const uint16_t *t;
+  template <int PH>  // PH = x & 3
   __device__ __forceinline__ int top(int x, int y) const {      // y = 4i - 1
-    return LAT ? t[((y + 1) >> 2) * kLatRowPitch + x + kColOff] : t[tidx(x, y)];
+    return LAT ? t[((y + 1) >> 2) * kLatRowPitch + x + kColOff] : t[tidx(x, y)] - (int)kBiasD[1][PH];
   }
   __device__ __forceinline__ uint2 top4(int x, int y) const {   // y = 4i - 1, x = 4k
-    return *reinterpret_cast<const uint2 *>(t + (LAT ? ((y + 1) >> 2) * kLatRowPitch + x + kColOff : tidx(x, y)));
+    const uint2 v = *reinterpret_cast<const uint2 *>(t + (LAT ? ((y + 1) >> 2) * kLatRowPitch + x + kColOff : tidx(x, y)));
+    return LAT ? v : make_uint2(v.x - bias_word(3, 0), v.y - bias_word(3, 2));
   }
   __device__ __forceinline__ int left(int x, int y) const {     // x = 4i - 1
-    return LAT ? t[16 * kLatRowPitch + ((x + 1) >> 2) * kLatColPitch + y + 1] : t[tidx(x, y)];
+    return LAT ? t[16 * kLatRowPitch + ((x + 1) >> 2) * kLatColPitch + y + 1] : t[tidx(x, y)] - (int)kBiasD[0][3];
   }
 };
 
@@ -188,7 +209,7 @@ __device__ __forceinline__ CuPos cu_pos(const Job &j, int fx0, int fy0, const Re
   c.top = fy0 + c.ly > 0;
   c.left = fx0 + c.lx > 0;
   c.padT = c.left ? rt.left(c.lx - 1, c.ly) : 512;  // top edge: sample (x-1, 0)
-  c.padL = c.top ? rt.top(c.lx, c.ly - 1) : 512;    // left edge: sample (0, y-1)
+  c.padL = c.top ? rt.template top<0>(c.lx, c.ly - 1) : 512;    // left edge: sample (0, y-1)
   return c;
 }
 
@@ -204,8 +225,8 @@ __device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> 
   constexpr int dfT = W / G::RBS, l2T = ilog2c(dfT), rndT = dfT > 1 ? dfT / 2 : 0;
   constexpr int dfL = H / G::RBS, l2L = ilog2c(dfL), rndL = dfL > 1 ? dfL / 2 : 0;
   uint32_t redT[G::RBS], redL[G::RBS];
-#pragma unroll
-  for (int i = 0; i < G::RBS; i++) {
+  static_for<G::RBS>([&](auto i_c) {
+    constexpr int i = decltype(i_c)::value;
     uint32_t s = 0;
     if constexpr (dfT >= 4) {
 #pragma unroll
@@ -214,15 +235,17 @@ __device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> 
         s += (v.x & 0xffff) + (v.x >> 16) + (v.y & 0xffff) + (v.y >> 16);
       }
     } else {
-#pragma unroll
-      for (int t = 0; t < dfT; t++) s += rt.top(c.lx + i * dfT + t, c.ly - 1);
+      static_for<dfT>([&](auto t_c) {
+        constexpr int off = i * dfT + decltype(t_c)::value;
+        s += rt.template top<off & 3>(c.lx + off, c.ly - 1);
+      });
     }
     redT[i] = c.top ? (s + rndT) >> l2T : c.padT;
     uint32_t l = 0;
 #pragma unroll
     for (int t = 0; t < dfL; t++) l += rt.left(c.lx - 1, c.ly + i * dfL + t);
     redL[i] = c.left ? (l + rndL) >> l2L : c.padL;
-  }
+  });
   constexpr uint32_t kBias = 0x64006400u;  // f16 1024.0 in both halves
   uint4 e;
   if constexpr (G::RBS == 4) {
@@ -239,56 +262,74 @@ __device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> 
 }
 
 struct BlockAcc {
-  s2 t[16];      // row-transformed residual
-  uint32_t pos;  // sum of max(d, 0), both modes packed (see block_finish for the bound)
+  uint32_t t[16];  // row-transformed biased residual (both modes, 16-bit halves)
+  uint32_t pos;    // sum of max(d, 0), both modes packed (see block_finish for the bound)
 };
 
 __device__ __forceinline__ uint32_t as_u32(s2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t as_u32(u2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ u2 as_u2(uint32_t v) { return __builtin_bit_cast(u2, v); }
 
-// One residual row of a 4x4 block: d = orig - pred, positive-part sum, row butterflies.
-__device__ __forceinline__ void block_row(BlockAcc &b, int i, const s2 (&prow)[4], uint2 orow) {
+// One residual row i of a 4x4 block: d' = o' - p = d + kBiasD[i & 1][c] (o' is the biased
+// staged sample, splat over both modes), the positive-part sum max(d, 0) = sat(d' - bias)
+// (v_pk_sub_u16 clamp), and the row butterflies as carry-free 32-bit adds / subtracts.
+template <int I>
+__device__ __forceinline__ void block_row(BlockAcc &b, const s2 (&prow)[4], uint2 orow) {
+  constexpr const uint32_t *B = kBiasD[I & 1];
   const s2 o01 = as_s2(orow.x), o23 = as_s2(orow.y);
-  const s2 d0 = s2{o01.x, o01.x} - prow[0], d1 = s2{o01.y, o01.y} - prow[1];
-  const s2 d2 = s2{o23.x, o23.x} - prow[2], d3 = s2{o23.y, o23.y} - prow[3];
-  const uint32_t p0 = as_u32(smax(d0, splat(0))), p1 = as_u32(smax(d1, splat(0)));
-  const uint32_t p2 = as_u32(smax(d2, splat(0))), p3 = as_u32(smax(d3, splat(0)));
-  b.pos = i == 0 ? p0 + p1 + p2 + p3 : b.pos + p0 + p1 + p2 + p3;
-  const s2 s0 = d0 + d1, s1 = d0 - d1, s2_ = d2 + d3, s3 = d2 - d3;
-  b.t[4 * i + 0] = s0 + s2_;
-  b.t[4 * i + 1] = s1 + s3;
-  b.t[4 * i + 2] = s0 - s2_;
-  b.t[4 * i + 3] = s1 - s3;
+  const uint32_t d0 = as_u32(s2{o01.x, o01.x} - prow[0]), d1 = as_u32(s2{o01.y, o01.y} - prow[1]);
+  const uint32_t d2 = as_u32(s2{o23.x, o23.x} - prow[2]), d3 = as_u32(s2{o23.y, o23.y} - prow[3]);
+  const uint32_t p0 = as_u32(__builtin_elementwise_sub_sat(as_u2(d0), (u2){(unsigned short)B[0], (unsigned short)B[0]}));
+  const uint32_t p1 = as_u32(__builtin_elementwise_sub_sat(as_u2(d1), (u2){(unsigned short)B[1], (unsigned short)B[1]}));
+  const uint32_t p2 = as_u32(__builtin_elementwise_sub_sat(as_u2(d2), (u2){(unsigned short)B[2], (unsigned short)B[2]}));
+  const uint32_t p3 = as_u32(__builtin_elementwise_sub_sat(as_u2(d3), (u2){(unsigned short)B[3], (unsigned short)B[3]}));
+  b.pos = I == 0 ? p0 + p1 + p2 + p3 : b.pos + p0 + p1 + p2 + p3;
+  const uint32_t s0 = d0 + d1, s1 = d0 - d1, s2_ = d2 + d3, s3 = d2 - d3;
+  b.t[4 * I + 0] = s0 + s2_;
+  b.t[4 * I + 1] = s1 + s3;
+  b.t[4 * I + 2] = s0 - s2_;
+  b.t[4 * I + 3] = s1 - s3;
+}
+
+// max(|a|, |b|) of two column-stage values sharing the bias `beta` (both halves):
+// max(max(a', b'), 2 beta - min(a', b')) - beta, unsigned compares on the biased values.
+template <uint32_t BETA>
+__device__ __forceinline__ uint32_t fold_pair(uint32_t a, uint32_t b) {
+  static_assert(2 * BETA < 65536, "bias");
+  const u2 mx = __builtin_elementwise_max(as_u2(a), as_u2(b)), mn = __builtin_elementwise_min(as_u2(a), as_u2(b));
+  const uint32_t ng = splat32(2 * BETA) - as_u32(mn);
+  return as_u32(__builtin_elementwise_max(mx, as_u2(ng))) - splat32(BETA);
 }
 
 // SAD and SATD of the block for both modes (packed 16-bit).
 // d = orig - pred in [-1023, 1023].  Hadamard intermediates: rows <= 4092, column sums
-// <= 8184, DC <= 16368 -- all int16.  SATD per block (kernel_aux_functions.cl:142-249):
+// <= 8184, DC <= 16368.  SATD per block (kernel_aux_functions.cl:142-249):
 //   (sum_k |c_k| - |c_0| + (|c_0| >> 2) + 1) >> 1.
 // The last butterfly is folded with |a+b| + |a-b| = 2 max(|a|, |b|), so with T = sum of
-// the seven non-DC pair maxima and U = |AC0| + (|DC| >> 2):  satd = T + ((U + 1) >> 1).
+// the seven non-DC pair maxima and U = |AC0| + (|DC| >> 2):  satd = T + ((U + 1) >> 1),
+// where |AC0| = 2 max(|u0|, |u2|) - |DC| for the column-0 pair (DC = u0 + u2, AC0 = u0 - u2).
 // By Parseval (||c||_2 = 4 ||d||_2) satd <= 32736 and T <= satd, so u16 holds both.
 // SAD = sum |d| = 2 * sum max(d, 0) - DC <= 16368, exact in 16 bits for the same reason.
-// Sums of non-negative packed halves that stay below 2^16 (pos, T) use plain 32-bit adds
-// (v_add3_u32: no carry crosses the halves).
+// Sums of non-negative packed halves that stay below 2^16 are plain 32-bit adds.
 __device__ __forceinline__ void block_finish(const BlockAcc &b, u2 &sad, u2 &satd) {
-  uint32_t T = 0;
-  s2 dc = splat(0), ac = splat(0);
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const s2 u0 = b.t[c] + b.t[4 + c], u1 = b.t[c] - b.t[4 + c];
-    const s2 u2_ = b.t[8 + c] + b.t[12 + c], u3 = b.t[8 + c] - b.t[12 + c];
-    if (c == 0) {
-      dc = u0 + u2_;
-      ac = u0 - u2_;
+  uint32_t T = 0, m0 = 0;
+  s2 dc = splat(0);
+  static_for<4>([&](auto c_c) {
+    constexpr int c = decltype(c_c)::value;
+    const uint32_t u0 = b.t[c] + b.t[4 + c], u1 = b.t[c] - b.t[4 + c];
+    const uint32_t u2_ = b.t[8 + c] + b.t[12 + c], u3 = b.t[8 + c] - b.t[12 + c];
+    T += fold_pair<kBiasQ>(u1, u3);
+    if constexpr (c == 0) {
+      m0 = fold_pair<kBiasP[0]>(u0, u2_);
+      dc = as_s2(u0) - as_s2(splat32(2 * kBiasP[0]) - u2_);  // u0 + u2 - 2 bias, signed
     } else {
-      T += as_u32(smax(smax(u0, u2_), splat(0) - smin(u0, u2_)));
+      T += fold_pair<kBiasP[c]>(u0, u2_);
     }
-    T += as_u32(smax(smax(u1, u3), splat(0) - smin(u1, u3)));
-  }
-  const s2 adc = smax(dc, splat(0) - dc), aac = smax(ac, splat(0) - ac);
-  const u2 U = as_u2(aac) + (as_u2(adc) >> (u2){2, 2});
-  satd = __builtin_bit_cast(u2, T) + ((U + (u2){1, 1}) >> (u2){1, 1});
-  sad = as_u2(as_s2(b.pos << 1) - dc);
+  });
+  const s2 adc = smax(dc, splat(0) - dc);
+  const uint32_t U = m0 + m0 - as_u32(adc) + as_u32(as_u2(adc) >> (u2){2, 2});
+  satd = as_u2(T + as_u32(as_u2(U + 0x00010001u) >> (u2){1, 1}));
+  sad = as_u2(as_s2(b.pos + b.pos) - dc);
 }
 
 // Packed block results -> 32-bit per-mode accumulators.
@@ -402,12 +443,12 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
     BlockAcc b;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
+    static_for<4>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
       s2 prow[4];
       red.row4(i, 0, prow);
-      block_row(b, i, prow, orig(i));
-    }
+      block_row<i>(b, prow, orig(i));
+    });
     u2 sad, satd;
     block_finish(b, sad, satd);
     acc.add(sad, satd);
@@ -418,12 +459,12 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
     for (int bi = 0; bi < G::KV / 4; bi++) {
       const int by = k0 / 4 + bi;
       BlockAcc b;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
+      static_for<4>([&](auto i_c) {
+        constexpr int i = decltype(i_c)::value;
         s2 prow[4];
         anchor_row<W, H>(red, 4 * by + i, x0, prow);
-        block_row(b, i, prow, orig(4 * by + i));
-      }
+        block_row<i>(b, prow, orig(4 * by + i));
+      });
       u2 sad, satd;
       block_finish(b, sad, satd);
       acc.add(sad, satd);
@@ -438,18 +479,18 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
     for (int bi = 0; bi < NBLK; bi++) {
       const int by = k0 / 2 + bi;
       BlockAcc b;
-#pragma unroll
-      for (int hh = 0; hh < 2; hh++) {
+      static_for<2>([&](auto hh_c) {
+        constexpr int hh = decltype(hh_c)::value;
         const int k = 2 * by + hh;
         s2 next[4], mid[4];
         anchor_row<W, H>(red, k, x0, next);
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) mid[cc] = avg_round(prev[cc], next[cc]);
-        block_row(b, 2 * hh, mid, orig(2 * k));
-        block_row(b, 2 * hh + 1, next, orig(2 * k + 1));
+        block_row<2 * hh>(b, mid, orig(2 * k));
+        block_row<2 * hh + 1>(b, next, orig(2 * k + 1));
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
-      }
+      });
       u2 sad, satd;
       block_finish(b, sad, satd);
       acc.add(sad, satd);
@@ -480,7 +521,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
             if constexpr (o == G::UV) prow[cc] = next[cc];
             else prow[cc] = as_s2(pk_mad_c<o>(delta[cc], base[cc]) >> (u2){G::LV, G::LV});
           }
-          block_row(b, i, prow, orig(k * G::UV + 4 * bi + i));
+          block_row<i>(b, prow, orig(k * G::UV + 4 * bi + i));
         });
         u2 sad, satd;
         block_finish(b, sad, satd);
@@ -693,9 +734,9 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   }
 }
 
-// Stage the quadrant window (rows -1..63, columns -4..63) of one frame into LDS.  Samples
-// outside the frame read as 0; they only feed CUs whose results are discarded or padding
-// branches that never select them.
+// Stage the quadrant window (rows -1..63, columns -4..63) of one frame into LDS, each
+// sample plus its residual bias (kBiasD).  Samples outside the frame read as 0 (+ bias);
+// they only feed CUs whose results are discarded or padding branches that never select them.
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
                                            int x0, int y0) {
   constexpr int kChunks = kPitch / 4;  // 17 chunks of 4 samples per row
@@ -705,6 +746,10 @@ __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame,
     uint2 v = make_uint2(0, 0);
     if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
       v = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
+    // residual bias of the sample's 4x4-block position (quadrant y = row - 1, x = 4ch - 4)
+    const uint32_t odd = (row - 1) & 1;
+    v.x += odd ? bias_word(1, 0) : bias_word(0, 0);
+    v.y += odd ? bias_word(1, 2) : bias_word(0, 2);
     *reinterpret_cast<uint2 *>(dst + row * kPitch + 4 * ch) = v;
   }
 }
