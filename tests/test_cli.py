@@ -203,3 +203,54 @@ def test_raw_inputs_binary_log_and_topk(gpu_available, tmp_path):
                         assert lst == exp
                     k += 1
     assert set(shapes) == {key[2] for key in got}
+
+
+@pytest.mark.gpu
+@needs_cli
+def test_streaming_chunks_multi_device(gpu_available, tmp_path):
+    """More frames than one chunk (--BatchFrames 2 over two engines: chunks of 4 frames,
+    the last one partial): frames are read, searched and written chunk by chunk through the
+    3-slot pipeline.  The log of every frame (--AllFrames), the binary log with SAD / SATD
+    (written out of order into its three regions) and the decision rows must equal the
+    oracle's, frame by frame and in order."""
+    W, H, N = 128, 136, 7
+    frames = synth_frames(W, H, N, 0xC14, 1)
+    write_csv(tmp_path / "in.csv", frames)
+    prefix = str(tmp_path / "out")
+    r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / "in.csv"), "-l", prefix, "--AllFrames",
+             "--ReportSadSatd", "--BatchFrames", "2", "--DeviceIndex", "0,0", "--BinaryLog", prefix + ".bin",
+             "--BestModes", prefix + "_best.csv"])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert [int(x) for x in re.findall(r"Current frame (\d+)", r.stdout)] == list(range(N))
+    want = [tuple(mask_unavailable(t, W, H) for t in O.search(frames[f], want_sad_satd=True)) for f in range(N)]
+    log = b"".join(reference_log(c, W, s, t).split(b"\n", 1)[1] if f else reference_log(c, W, s, t)
+                   for f, (c, s, t) in enumerate(want))
+    assert open(prefix + ".csv", "rb").read() == log
+    b = layout.read_binary_log(prefix + ".bin")
+    assert b["frames"] == N
+    for key, i in (("cost", 0), ("sad", 1), ("satd", 2)):
+        assert np.array_equal(np.asarray(b[key]), np.stack([w[i] for w in want])), key
+    import csv
+    rows = list(csv.DictReader(open(prefix + "_best.csv")))
+    assert len(rows) == N * layout.num_ctus(W, H) * layout.CUS_PER_CTU
+    assert [int(x["Frame"]) for x in rows[::layout.CUS_PER_CTU]] == sorted(
+        [f for f in range(N) for _ in range(layout.num_ctus(W, H))])
+    n = layout.num_ctus(W, H)
+    for f in range(N):
+        bm, bc = layout.best_modes(want[f][0], n)
+        got = rows[f * n * layout.CUS_PER_CTU:(f + 1) * n * layout.CUS_PER_CTU]
+        assert [int(x["Cost"]) for x in got] == bc.tolist()
+
+
+@pytest.mark.gpu
+@needs_cli
+def test_truncated_input_fails(gpu_available, tmp_path):
+    """A CSV with fewer frames than -f asks for: exit 1 with the reference's message
+    (main.cpp:366-368 perror), even when the shortfall is in a later chunk."""
+    W, H = 128, 128
+    frames = synth_frames(W, H, 2, 0xC15, 0)
+    write_csv(tmp_path / "in.csv", frames)
+    r = run(["-f", "5", "-s", f"{W}x{H}", "-o", str(tmp_path / "in.csv"), "-l", str(tmp_path / "o"),
+             "--BatchFrames", "1"])
+    assert r.returncode == 1
+    assert "error while opening samples files" in r.stderr

@@ -31,8 +31,15 @@
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "mipgpu.h"
 
@@ -199,8 +206,14 @@ struct Pinned {
   T &operator[](size_t i) { return p[i]; }
 };
 
-// CSV reader (main.cpp:364-384 format): the file is read whole, line starts are indexed,
-// and the H*n rows are parsed by `threads` threads.
+// Sequential frame source (main.cpp:364-384 reads the whole CSV before the search; here
+// frames are read chunk by chunk while earlier chunks are searched and logged, so host
+// memory does not grow with the sequence length).
+//  * CSV: the file is memory-mapped; per chunk the H*n line starts are indexed and the rows
+//    parsed by `threads` threads (H lines of W comma-separated samples per frame).
+//  * raw: `luma_only` = consecutive W x H little-endian 16-bit frames; otherwise planar
+//    4:2:0 with 16-bit samples (yuv420p10le), whose two chroma planes (W/2 x H/2 each) are
+//    skipped.
 bool parse_row(const char *p, const char *end, int W, uint16_t *out) {
   for (int x = 0; x < W; x++) {
     while (p < end && (*p == ' ' || *p == '\r')) p++;
@@ -215,45 +228,74 @@ bool parse_row(const char *p, const char *end, int W, uint16_t *out) {
   return true;
 }
 
-bool read_frames(const std::string &path, int W, int H, int n, uint16_t *out, int threads) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) return false;
-  std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  const size_t rows = (size_t)H * n;
-  std::vector<size_t> start;
-  start.reserve(rows + 1);
-  for (size_t pos = 0; start.size() < rows && pos < data.size();) {
-    start.push_back(pos);
-    const void *nl = memchr(data.data() + pos, '\n', data.size() - pos);
-    pos = nl ? (size_t)((const char *)nl - data.data()) + 1 : data.size();
+class FrameSource {
+ public:
+  ~FrameSource() {
+    if (map_ && map_ != MAP_FAILED) munmap(map_, size_);
+    if (fd_ >= 0) close(fd_);
+    if (raw_) fclose(raw_);
   }
-  if (start.size() < rows) return false;
-  start.push_back(data.size());
-  std::vector<char> ok(std::max(1, threads), 1);
-  std::vector<std::thread> pool;
-  for (int t = 0; t < (int)ok.size(); t++)
-    pool.emplace_back([&, t] {
-      for (size_t r = t; r < rows; r += ok.size())
-        if (!parse_row(data.data() + start[r], data.data() + start[r + 1], W, out + r * W)) ok[t] = 0;
-    });
-  for (auto &th : pool) th.join();
-  return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
-}
+  bool open(const std::string &path, const std::string &fmt, int W, int H, int threads) {
+    W_ = W, H_ = H, threads_ = std::max(1, threads);
+    csv_ = fmt == "csv";
+    if (!csv_) {
+      luma_only_ = fmt == "u16";
+      raw_ = fopen(path.c_str(), "rb");
+      return raw_ != nullptr;
+    }
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) return false;
+    struct stat st;
+    if (fstat(fd_, &st) != 0) return false;
+    size_t sz = (size_t)st.st_size;
+    if (sz == 0) return true;  // empty file: the first read fails
+    map_ = mmap(nullptr, sz, PROT_READ, MAP_PRIVATE, fd_, 0);
+    if (map_ == MAP_FAILED) return false;
+    size_ = sz;
+    madvise(map_, size_, MADV_SEQUENTIAL);
+    return true;
+  }
+  // Next n frames into out (n * W * H samples).
+  bool read(int n, uint16_t *out) {
+    const size_t fs = (size_t)W_ * H_;
+    if (!csv_) {
+      const size_t chroma = luma_only_ ? 0 : 2 * (size_t)(W_ / 2) * (H_ / 2);
+      for (int i = 0; i < n; i++) {
+        if (fread(out + i * fs, 2, fs, raw_) != fs) return false;
+        if (chroma && fseek(raw_, (long)(chroma * 2), SEEK_CUR) != 0) return false;
+      }
+      return true;
+    }
+    const char *data = static_cast<const char *>(map_);
+    const size_t rows = (size_t)H_ * n;
+    start_.clear();
+    for (size_t r = 0; r < rows; r++) {
+      if (pos_ >= size_) return false;
+      start_.push_back(pos_);
+      const void *nl = memchr(data + pos_, '\n', size_ - pos_);
+      pos_ = nl ? (size_t)((const char *)nl - data) + 1 : size_;
+    }
+    start_.push_back(pos_);
+    std::vector<char> ok(threads_, 1);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads_; t++)
+      pool.emplace_back([&, t] {
+        for (size_t r = t; r < rows; r += threads_)
+          if (!parse_row(data + start_[r], data + start_[r + 1], W_, out + r * W_)) ok[t] = 0;
+      });
+    for (auto &th : pool) th.join();
+    return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
+  }
 
-// Raw frames: `luma_only` = consecutive W x H little-endian 16-bit frames; otherwise planar
-// 4:2:0 with 16-bit samples (yuv420p10le), whose two chroma planes (W/2 x H/2 each) are skipped.
-bool read_raw_frames(const std::string &path, int W, int H, int n, bool luma_only, uint16_t *out) {
-  FILE *f = fopen(path.c_str(), "rb");
-  if (!f) return false;
-  const size_t fs = (size_t)W * H, chroma = luma_only ? 0 : 2 * (size_t)(W / 2) * (H / 2);
-  bool ok = true;
-  for (int i = 0; i < n && ok; i++) {
-    ok = fread(out + i * fs, 2, fs, f) == fs;
-    if (ok && chroma) ok = fseek(f, (long)(chroma * 2), SEEK_CUR) == 0;
-  }
-  fclose(f);
-  return ok;
-}
+ private:
+  int W_ = 0, H_ = 0, threads_ = 1;
+  bool csv_ = true, luma_only_ = true;
+  FILE *raw_ = nullptr;
+  int fd_ = -1;
+  void *map_ = nullptr;
+  size_t size_ = 0, pos_ = 0;
+  std::vector<size_t> start_;
+};
 
 std::string input_format(const Options &o) {
   if (o.input_format != "auto") return o.input_format;
@@ -352,16 +394,10 @@ int main(int argc, char **argv) {
     std::cout << "  [!] ERROR: Input resolution \"" << o.resolution << "\" not set properly" << std::endl;
     return 0;
   }
-  Pinned<uint16_t> frames;
-  if (!frames.alloc((size_t)W * H * std::max(1, o.frames))) {
-    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
-    return 1;
-  }
   const std::string fmt = input_format(o);
   const int threads = o.threads > 0 ? o.threads : (int)std::max(1u, std::thread::hardware_concurrency());
-  const bool read_ok = fmt == "csv" ? read_frames(o.input, W, H, o.frames, frames.data(), threads)
-                                    : read_raw_frames(o.input, W, H, o.frames, fmt == "u16", frames.data());
-  if (!read_ok) {
+  FrameSource src;
+  if (!src.open(o.input, fmt, W, H, threads)) {
     perror("error while opening samples files");
     return 1;
   }
@@ -387,48 +423,11 @@ int main(int argc, char **argv) {
     }
     engines.push_back(e);
   }
-  const size_t cpf = (size_t)nctus * MIP_COSTS_PER_CTU_ABI, upf = (size_t)nctus * MIP_CUS_PER_CTU_ABI * o.topk;
-  Pinned<int32_t> cost, sad, satd, best_cost;
-  Pinned<uint8_t> best;
-  bool ok = cost.alloc(cpf * o.frames);
-  if (o.sad_satd) ok = ok && sad.alloc(cpf * o.frames) && satd.alloc(cpf * o.frames);
-  if (!o.best_modes.empty()) ok = ok && best.alloc(upf * o.frames) && best_cost.alloc(upf * o.frames);
-  if (!ok) {
-    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
-    destroy_all();
-    return 1;
-  }
-
-  // Frames sharded over the engines: contiguous ranges, one host thread per device.
   const int ndev = (int)engines.size();
   const size_t fs = (size_t)W * H;
-  std::vector<int> rcs(ndev, 0);
-  std::vector<std::string> errs(ndev);
-  const auto t0 = std::chrono::steady_clock::now();  // save_startTime, main.cpp:568
-  {
-    std::vector<std::thread> workers;
-    for (int d = 0; d < ndev; d++) {
-      const int f0 = (int)((long long)o.frames * d / ndev), f1 = (int)((long long)o.frames * (d + 1) / ndev);
-      if (f1 <= f0) continue;
-      workers.emplace_back([&, d, f0, f1] {
-        rcs[d] = mip_search_frames(engines[d], frames.data() + f0 * fs, nullptr, f1 - f0, cost.data() + f0 * cpf,
-                                   best.empty() ? nullptr : best.data() + f0 * upf,
-                                   best.empty() ? nullptr : best_cost.data() + f0 * upf,
-                                   o.sad_satd ? sad.data() + f0 * cpf : nullptr,
-                                   o.sad_satd ? satd.data() + f0 * cpf : nullptr);
-        if (rcs[d] != 0) errs[d] = mip_last_error();
-      });
-    }
-    for (auto &w : workers) w.join();
-  }
-  const auto t1 = std::chrono::steady_clock::now();  // save_finishTime, main.cpp:1249
-  for (int d = 0; d < ndev; d++)
-    if (rcs[d] != 0) {
-      std::cout << "  [!] ERROR: device " << o.devices[d] << ": " << errs[d] << std::endl;
-      destroy_all();
-      return 1;
-    }
-  for (int f = 0; f < o.frames; f++) std::cout << "Current frame " << f << std::endl;
+  const size_t cpf = (size_t)nctus * MIP_COSTS_PER_CTU_ABI, upf = (size_t)nctus * MIP_CUS_PER_CTU_ABI * o.topk;
+  const int nlog = o.all_frames ? o.frames : std::min(1, o.frames);
+  const bool want_best = !o.best_modes.empty(), want_bin = !o.binary_log.empty();
 
   std::vector<ShapeInfo> shapes(47);
   for (int s = 0; s < 47; s++) {
@@ -439,58 +438,202 @@ int main(int argc, char **argv) {
     sh.y.resize(sh.ncu);
     for (int cu = 0; cu < sh.ncu; cu++) mip_cu_position(s, cu, &sh.x[cu], &sh.y[cu]);
   }
-  // reportDistortionToFile=1 in the reference even when -l is not given (writes ".csv").
-  {
-    FILE *fp = fopen((o.prefix + ".csv").c_str(), "w");
-    if (!fp) { perror("cannot open cost log"); destroy_all(); return 1; }
-    fprintf(fp, "CTU,cuSizeName,W,H,CU,X,Y,Mode,SAD,SATD,minSadHad\n");
-    const int nlog = o.all_frames ? o.frames : std::min(1, o.frames);
-    for (int f = 0; f < nlog; f++)
-      write_cost_log(fp, shapes, nctus, W, cost.data() + f * cpf, o.sad_satd ? sad.data() + f * cpf : nullptr,
-                     o.sad_satd ? satd.data() + f * cpf : nullptr, threads);
-    fclose(fp);
+  // Output files.  reportDistortionToFile=1 in the reference even when -l is not given
+  // (writes ".csv").  Binary log header: "MIPC", version 1, width, height, frames, entries
+  // per frame, flags (bit 0: SAD and SATD tables follow the cost tables), reserved; then
+  // int32 little-endian tables (costs of every frame, then SAD, then SATD).
+  FILE *log_fp = fopen((o.prefix + ".csv").c_str(), "w");
+  if (!log_fp) { perror("cannot open cost log"); destroy_all(); return 1; }
+  fprintf(log_fp, "CTU,cuSizeName,W,H,CU,X,Y,Mode,SAD,SATD,minSadHad\n");
+  FILE *best_fp = nullptr, *bin_fp = nullptr;
+  if (want_best) {
+    best_fp = fopen(o.best_modes.c_str(), "w");
+    if (!best_fp) { perror("cannot open best-mode file"); destroy_all(); return 1; }
+    if (o.topk == 1) fprintf(best_fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,Transposed,Cost\n");
+    else fprintf(best_fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,Rank,Mode,Transposed,Cost\n");
   }
-  if (!o.best_modes.empty()) {
-    FILE *fp = fopen(o.best_modes.c_str(), "w");
-    if (!fp) { perror("cannot open best-mode file"); destroy_all(); return 1; }
-    const int K = o.topk;
-    if (K == 1) fprintf(fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,Transposed,Cost\n");
-    else fprintf(fp, "Frame,CTU,cuSizeName,W,H,CU,X,Y,Rank,Mode,Transposed,Cost\n");
-    const int ctu_cols = (W + 127) / 128;
-    for (int f = 0; f < o.frames; f++)
-      for (int ctu = 0, k = 0; ctu < nctus; ctu++)
-        for (const ShapeInfo &sh : shapes)
-          for (int cu = 0; cu < sh.ncu; cu++, k++) {
-            const size_t i0 = f * upf + ((size_t)ctu * MIP_CUS_PER_CTU_ABI + (k % MIP_CUS_PER_CTU_ABI)) * K;
-            const int x = 128 * (ctu % ctu_cols) + sh.x[cu], y = 128 * (ctu / ctu_cols) + sh.y[cu];
-            for (int r = 0; r < K; r++) {
-              const int m = best[i0 + r];
-              if (K > 1 && m == 0xff && best[i0] != 0xff) break;  // past the CU's modes
-              if (K == 1)
-                fprintf(fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x, y,
-                        m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
-              else
-                fprintf(fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x, y, r,
-                        m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
-              if (m == 0xff) break;  // unavailable CU: one row
-            }
-          }
-    fclose(fp);
-  }
-  if (!o.binary_log.empty()) {
-    // header: "MIPC", version 1, width, height, frames, entries per frame, flags (bit 0: SAD
-    // and SATD tables follow the cost tables), reserved; then int32 little-endian tables
-    FILE *fp = fopen(o.binary_log.c_str(), "wb");
-    if (!fp) { perror("cannot open binary log"); destroy_all(); return 1; }
+  if (want_bin) {
+    bin_fp = fopen(o.binary_log.c_str(), "wb");
+    if (!bin_fp) { perror("cannot open binary log"); destroy_all(); return 1; }
     const uint32_t hdr[8] = {0x4350494du, 1u, (uint32_t)W, (uint32_t)H, (uint32_t)o.frames, (uint32_t)cpf,
                              o.sad_satd ? 1u : 0u, 0u};
-    bool wok = fwrite(hdr, 4, 8, fp) == 8 && fwrite(cost.data(), 4, cpf * o.frames, fp) == cpf * o.frames;
-    if (o.sad_satd)
-      wok = wok && fwrite(sad.data(), 4, cpf * o.frames, fp) == cpf * o.frames &&
-            fwrite(satd.data(), 4, cpf * o.frames, fp) == cpf * o.frames;
-    if (fclose(fp) != 0 || !wok) { perror("writing binary log"); destroy_all(); return 1; }
+    if (fwrite(hdr, 4, 8, bin_fp) != 8) { perror("writing binary log"); destroy_all(); return 1; }
   }
-  const long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count();
+
+  // Chunk pipeline over kSlots buffer slots: a reader thread fills a slot's frames, this
+  // thread searches them (frames sharded over the engines, one host thread per device),
+  // a writer thread emits the chunk's log rows / decision rows / binary tables in frame
+  // order and frees the slot.  Host memory is bounded by kSlots chunks.
+  constexpr int kSlots = 3;
+  const int chunk = std::max(1, opts.max_batch) * ndev;
+  const int nchunks = o.frames > 0 ? (o.frames + chunk - 1) / chunk : 0;
+  struct Slot {
+    Pinned<uint16_t> in;
+    Pinned<int32_t> cost, sad, satd, best_cost;
+    Pinned<uint8_t> best;
+    int state = 0;  // 0 free, 1 frames read, 2 searched
+  };
+  std::vector<Slot> slots(kSlots);
+  const bool cost_all = want_bin || o.all_frames;
+  bool ok = true;
+  for (Slot &sl : slots) {
+    const size_t n = (size_t)std::min(chunk, std::max(1, o.frames));
+    ok = ok && sl.in.alloc(n * fs) && sl.cost.alloc((cost_all ? n : 1) * cpf);
+    if (o.sad_satd) ok = ok && sl.sad.alloc((cost_all ? n : 1) * cpf) && sl.satd.alloc((cost_all ? n : 1) * cpf);
+    if (want_best) ok = ok && sl.best.alloc(n * upf) && sl.best_cost.alloc(n * upf);
+  }
+  if (!ok) {
+    std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
+    destroy_all();
+    return 1;
+  }
+  std::mutex mu;
+  std::condition_variable cv;
+  bool read_failed = false, search_failed = false, write_failed = false;
+  auto wait_state = [&](int s, int st) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return slots[s].state == st || read_failed || search_failed || write_failed; });
+    return slots[s].state == st;
+  };
+  auto set_state = [&](int s, int st) {
+    { std::lock_guard<std::mutex> lk(mu); slots[s].state = st; }
+    cv.notify_all();
+  };
+  auto fail = [&](bool &flag) {
+    { std::lock_guard<std::mutex> lk(mu); flag = true; }
+    cv.notify_all();
+  };
+  auto chunk_range = [&](int c, int &f0, int &n) { f0 = c * chunk; n = std::min(chunk, o.frames - f0); };
+
+  std::thread reader([&] {
+    for (int c = 0; c < nchunks; c++) {
+      const int s = c % kSlots;
+      if (!wait_state(s, 0)) return;
+      int f0, n;
+      chunk_range(c, f0, n);
+      if (!src.read(n, slots[s].in.data())) return fail(read_failed);
+      set_state(s, 1);
+    }
+  });
+  const int ctu_cols = (W + 127) / 128;
+  std::thread writer([&] {
+    for (int c = 0; c < nchunks; c++) {
+      const int s = c % kSlots;
+      if (!wait_state(s, 2)) return;
+      Slot &sl = slots[s];
+      int f0, n;
+      chunk_range(c, f0, n);
+      bool wok = true;
+      for (int i = 0; i < n; i++) {
+        const int f = f0 + i;
+        const size_t co = cost_all ? i * cpf : 0;  // slot-local cost table of frame f
+        if (f < nlog)
+          write_cost_log(log_fp, shapes, nctus, W, sl.cost.data() + co, o.sad_satd ? sl.sad.data() + co : nullptr,
+                         o.sad_satd ? sl.satd.data() + co : nullptr, threads);
+        if (want_bin) {
+          const long long base = 32, tab = (long long)cpf * 4;
+          wok = wok && fseeko(bin_fp, base + f * tab, SEEK_SET) == 0 && fwrite(sl.cost.data() + co, 4, cpf, bin_fp) == cpf;
+          if (o.sad_satd)
+            wok = wok && fseeko(bin_fp, base + (o.frames + f) * tab, SEEK_SET) == 0 &&
+                  fwrite(sl.sad.data() + co, 4, cpf, bin_fp) == cpf &&
+                  fseeko(bin_fp, base + (2LL * o.frames + f) * tab, SEEK_SET) == 0 &&
+                  fwrite(sl.satd.data() + co, 4, cpf, bin_fp) == cpf;
+        }
+        if (want_best) {
+          const int K = o.topk;
+          const uint8_t *best = sl.best.data() + i * upf;
+          const int32_t *best_cost = sl.best_cost.data() + i * upf;
+          for (int ctu = 0, k = 0; ctu < nctus; ctu++)
+            for (const ShapeInfo &sh : shapes)
+              for (int cu = 0; cu < sh.ncu; cu++, k++) {
+                const size_t i0 = ((size_t)ctu * MIP_CUS_PER_CTU_ABI + (k % MIP_CUS_PER_CTU_ABI)) * K;
+                const int x = 128 * (ctu % ctu_cols) + sh.x[cu], y = 128 * (ctu / ctu_cols) + sh.y[cu];
+                for (int r = 0; r < K; r++) {
+                  const int m = best[i0 + r];
+                  if (K > 1 && m == 0xff && best[i0] != 0xff) break;  // past the CU's modes
+                  if (K == 1)
+                    fprintf(best_fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x, y,
+                            m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
+                  else
+                    fprintf(best_fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x,
+                            y, r, m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
+                  if (m == 0xff) break;  // unavailable CU: one row
+                }
+              }
+        }
+      }
+      if (!wok) return fail(write_failed);
+      set_state(s, 0);
+    }
+  });
+
+  // "Elapsed time from writing samples to reading distortion" (main_aux_functions.h:192-211,
+  // 908-914): the summed wall time of the chunks' device round trips (H2D, search, D2H);
+  // file reading and log writing, outside that window in the reference, overlap it here.
+  std::chrono::steady_clock::duration search_time{};
+  std::vector<int> rcs(ndev, 0);
+  std::vector<std::string> errs(ndev);
+  for (int c = 0; c < nchunks && !search_failed; c++) {
+    const int s = c % kSlots;
+    if (!wait_state(s, 1)) break;
+    Slot &sl = slots[s];
+    int f0, n;
+    chunk_range(c, f0, n);
+    const bool need_cost = cost_all || f0 < nlog;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> workers;
+    for (int d = 0; d < ndev; d++) {
+      const int a = (int)((long long)n * d / ndev), b = (int)((long long)n * (d + 1) / ndev);
+      if (b <= a) continue;
+      // costs: every frame when all are logged / binary-logged, else only the chunk's
+      // first frame (frame 0, the reference's log) and only for the engine that has it
+      const bool dc = need_cost && (cost_all || a == 0);
+      const size_t co = cost_all ? a * cpf : 0;
+      const int nb = cost_all || !dc ? b - a : 1;
+      workers.emplace_back([&, d, a, b, dc, co, nb] {
+        rcs[d] = 0;
+        if (!dc || nb == b - a)
+          rcs[d] = mip_search_frames(engines[d], sl.in.data() + a * fs, nullptr, b - a, dc ? sl.cost.data() + co : nullptr,
+                                     want_best ? sl.best.data() + a * upf : nullptr,
+                                     want_best ? sl.best_cost.data() + a * upf : nullptr,
+                                     dc && o.sad_satd ? sl.sad.data() + co : nullptr,
+                                     dc && o.sad_satd ? sl.satd.data() + co : nullptr);
+        else  // the first frame's tables, then the rest without tables
+          rcs[d] = mip_search_frames(engines[d], sl.in.data() + a * fs, nullptr, 1, sl.cost.data(),
+                                     want_best ? sl.best.data() + a * upf : nullptr,
+                                     want_best ? sl.best_cost.data() + a * upf : nullptr,
+                                     o.sad_satd ? sl.sad.data() : nullptr, o.sad_satd ? sl.satd.data() : nullptr) ||
+                   (b - a > 1 &&
+                    mip_search_frames(engines[d], sl.in.data() + (a + 1) * fs, nullptr, b - a - 1, nullptr,
+                                      want_best ? sl.best.data() + (a + 1) * upf : nullptr,
+                                      want_best ? sl.best_cost.data() + (a + 1) * upf : nullptr, nullptr, nullptr));
+        if (rcs[d] != 0) errs[d] = mip_last_error();
+      });
+    }
+    for (auto &w : workers) w.join();
+    search_time += std::chrono::steady_clock::now() - t0;
+    for (int d = 0; d < ndev; d++)
+      if (rcs[d] != 0) {
+        std::cout << "  [!] ERROR: device " << o.devices[d] << ": " << errs[d] << std::endl;
+        fail(search_failed);
+      }
+    if (search_failed) break;
+    for (int i = 0; i < n; i++) std::cout << "Current frame " << f0 + i << std::endl;
+    set_state(s, 2);
+  }
+  reader.join();
+  writer.join();
+  fclose(log_fp);
+  if (best_fp) fclose(best_fp);
+  const bool bin_ok = !bin_fp || fclose(bin_fp) == 0;
+  if (read_failed) {
+    perror("error while opening samples files");
+    destroy_all();
+    return 1;
+  }
+  if (search_failed) { destroy_all(); return 1; }
+  if (write_failed || !bin_ok) { perror("writing binary log"); destroy_all(); return 1; }
+  const long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(search_time).count();
   printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n");
   printf("TIMING RESULTS (miliseconds)\n");
   printf("Elapsed time (ms) from writing samples to reading distortion (%dx), %ld\n", o.frames, ms);
