@@ -391,17 +391,18 @@ __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, s2 (&a
     const s2 before = red(k, kx - 1);
     const u2 delta = as_u2(after - before);
     const u2 base = pk_mad_cc<G::UH, G::UH / 2>(as_u2(before));
-    // the strip's 4 columns are phases o0+1..o0+4 of one window (o0 = 0 or 4 for UH = 8)
-    const int o0 = x0 & (G::UH - 1);
+    // the strip's 4 columns are phases o0+1..o0+4 of one window (o0 = 0 or 4 for UH = 8:
+    // it differs between neighbouring lanes, so it enters as data, base += o0 * delta,
+    // not as a branch)
+    u2 base0 = base;
+    if constexpr (G::UH == 8) {
+      const uint32_t o0 = splat32(x0 & (G::UH - 1));
+      asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(base0) : "v"(delta), "v"(o0), "v"(base));
+    }
     auto tap = [&](auto oc) {  // (o*delta + base) >> LH, o = oc + 1 + o0
       constexpr int c = decltype(oc)::value;
-      if constexpr (G::UH == 4) {
-        if constexpr (c == 3) return after;  // o = UH: the anchor itself
-        else return as_s2(pk_mad_c<c + 1>(delta, base) >> (u2){G::LH, G::LH});
-      } else {
-        const u2 v = o0 == 0 ? pk_mad_c<c + 1>(delta, base) : pk_mad_c<c + 5>(delta, base);
-        return as_s2(v >> (u2){G::LH, G::LH});
-      }
+      if constexpr (G::UH == 4 && c == 3) return after;  // o = UH: the anchor itself
+      else return as_s2(pk_mad_c<c + 1>(delta, base0) >> (u2){G::LH, G::LH});
     };
     a[0] = tap(std::integral_constant<int, 0>{});
     a[1] = tap(std::integral_constant<int, 1>{});
