@@ -389,25 +389,35 @@ __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, s2 (&a
     const int kx = x0 >> G::LH;
     const s2 after = red(k, kx);
     const s2 before = red(k, kx - 1);
-    const u2 delta = as_u2(after - before);
+    // Numerators n_o = base + o*delta walked incrementally: `delta` is the exact 32-bit
+    // difference of the packed pairs (after - before), so n += delta is one v_add_u32 that
+    // is exact on both halves (every n_o per half lies in [0, 8188]: no carry or borrow
+    // leaves the low half of the true sum).  v_add_u32 dual-issues on gfx950, the
+    // v_pk_mad_u16 it replaces does not (tools/dual_census.hip).
+    const uint32_t delta = as_u32(after) - as_u32(before);
     const u2 base = pk_mad_cc<G::UH, G::UH / 2>(as_u2(before));
     // the strip's 4 columns are phases o0+1..o0+4 of one window (o0 = 0 or 4 for UH = 8:
     // it differs between neighbouring lanes, so it enters as data, base += o0 * delta,
     // not as a branch)
-    u2 base0 = base;
+    uint32_t n = as_u32(base);
     if constexpr (G::UH == 8) {
+      // per-half differences for the packed multiply (the 32-bit difference carries the
+      // low half's borrow in its high half)
+      const u2 hdelta = as_u2(after - before);
       const uint32_t o0 = splat32(x0 & (G::UH - 1));
-      asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(base0) : "v"(delta), "v"(o0), "v"(base));
+      u2 base0;
+      asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(base0) : "v"(hdelta), "v"(o0), "v"(base));
+      n = as_u32(base0);
     }
-    auto tap = [&](auto oc) {  // (o*delta + base) >> LH, o = oc + 1 + o0
+    static_for<4>([&](auto oc) {  // (o*delta + base) >> LH, o = oc + 1 + o0
       constexpr int c = decltype(oc)::value;
-      if constexpr (G::UH == 4 && c == 3) return after;  // o = UH: the anchor itself
-      else return as_s2(pk_mad_c<c + 1>(delta, base0) >> (u2){G::LH, G::LH});
-    };
-    a[0] = tap(std::integral_constant<int, 0>{});
-    a[1] = tap(std::integral_constant<int, 1>{});
-    a[2] = tap(std::integral_constant<int, 2>{});
-    a[3] = tap(std::integral_constant<int, 3>{});
+      if constexpr (G::UH == 4 && c == 3) {
+        a[c] = after;  // o = UH: the anchor itself
+      } else {
+        n += delta;
+        a[c] = as_s2(as_u2(n) >> (u2){G::LH, G::LH});
+      }
+    });
   }
 }
 
@@ -497,19 +507,20 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
       acc.add(sad, satd);
     }
   } else {
-    // Vertical pass: row o (1..UV) of window k is (base + o*delta) >> LV with
-    // base = (prev << LV) + UV/2, the reference numerator, in [0, 8188]; o = UV gives the
-    // anchor itself.  16-bit wrap-around in o*delta cancels in the in-range sum.
+    // Vertical pass: row o (1..UV) of window k is n_o >> LV with n_o = base + o*delta,
+    // base = (prev << LV) + UV/2: the reference numerator, in [0, 8188] on both halves.  It
+    // is walked incrementally, n_o = n_{o-1} + delta, with delta the exact 32-bit
+    // difference of the packed pairs (see anchor_row); o = UV gives the anchor itself.
     constexpr int NB = G::UV / 4;  // blocks per window
 #pragma unroll 1
     for (int k = k0; k < k1; k++) {
       s2 next[4];
       anchor_row<W, H>(red, k, x0, next);
-      u2 delta[4], base[4];
+      uint32_t delta[4], num[4];
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) {
-        delta[cc] = as_u2(next[cc]) - as_u2(prev[cc]);
-        base[cc] = pk_mad_cc<G::UV, G::UV / 2>(as_u2(prev[cc]));
+        delta[cc] = as_u32(next[cc]) - as_u32(prev[cc]);
+        num[cc] = as_u32(pk_mad_cc<G::UV, G::UV / 2>(as_u2(prev[cc])));
       }
       static_for<NB>([&](auto bi_c) {
         constexpr int bi = decltype(bi_c)::value;
@@ -519,8 +530,12 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
           s2 prow[4];
 #pragma unroll
           for (int cc = 0; cc < 4; cc++) {
-            if constexpr (o == G::UV) prow[cc] = next[cc];
-            else prow[cc] = as_s2(pk_mad_c<o>(delta[cc], base[cc]) >> (u2){G::LV, G::LV});
+            if constexpr (o == G::UV) {
+              prow[cc] = next[cc];
+            } else {
+              num[cc] += delta[cc];
+              prow[cc] = as_s2(as_u2(num[cc]) >> (u2){G::LV, G::LV});
+            }
           }
           block_row<i>(b, prow, orig(k * G::UV + 4 * bi + i));
         });
