@@ -47,6 +47,18 @@ typedef _Float16 __attribute__((ext_vector_type(4))) h4;
 typedef float __attribute__((ext_vector_type(4))) f4;
 
 __constant__ mip_shape_desc c_shapes[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;
+// first CU (reference order inside a CTU) of every shape, for the decision-list kernel
+struct ShapeStarts {
+  uint16_t v[MIP_NUM_SHAPES + 1];
+};
+constexpr mip_shape_desc kShapesC[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;
+constexpr ShapeStarts make_shape_starts() {
+  ShapeStarts st{};
+  for (int i = 0; i < MIP_NUM_SHAPES; i++) st.v[i + 1] = (uint16_t)(st.v[i] + kShapesC[i].ncu);
+  return st;
+}
+static_assert(make_shape_starts().v[MIP_NUM_SHAPES] == MIP_CUS_PER_CTU, "shape table");
+__constant__ ShapeStarts c_shape_start = make_shape_starts();
 
 #ifndef MIP_ONLY_CLASS
 #define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
@@ -922,7 +934,10 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
   if (g >= a.total_cus) return;
   const int ctu = g / MIP_CUS_PER_CTU;
   int r = g - ctu * MIP_CUS_PER_CTU, s = 0;
-  while (r >= c_shapes[s].ncu) r -= c_shapes[s++].ncu;
+#pragma unroll
+  for (int step = 32; step; step >>= 1)  // last shape whose first CU is <= r
+    if (s + step < MIP_NUM_SHAPES && c_shape_start.v[s + step] <= r) s += step;
+  r -= c_shape_start.v[s];
   const mip_shape_desc sd = c_shapes[s];
   const int32_t *row = a.cost + (size_t)ctu * MIP_COSTS_PER_CTU + sd.cost_offset + (size_t)r * 2 * sd.modes;
   uint8_t *mo = a.best_mode ? a.best_mode + (size_t)g * a.k : nullptr;

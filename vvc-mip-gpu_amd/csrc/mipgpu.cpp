@@ -253,7 +253,12 @@ bool filter_valid(int f, int k) {
 struct mip_engine {
   int device = 0, width = 0, height = 0, nctus = 0, ctu_cols = 0;
   mip_opts opts{};
-  hipStream_t stream = nullptr, stream2 = nullptr;  // host API: two halves of the batch in flight
+  // Host API pipeline (mip_search_frames): `stream` computes, `stream2` uploads, `stream3`
+  // downloads; per buffer slot, events order upload -> compute -> download and a slot's
+  // reuse after its previous chunk (see mip_search_frames).
+  hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+  static constexpr int kHostSlots = 4;
+  hipEvent_t slot_up[kHostSlots] = {}, slot_comp[kHostSlots] = {}, slot_down[kHostSlots] = {};
   uint16_t *d_frames = nullptr, *d_refs = nullptr;
   int32_t *d_costs = nullptr, *d_sad = nullptr, *d_satd = nullptr, *d_best_cost = nullptr;
   uint8_t *d_best = nullptr;
@@ -361,6 +366,7 @@ int mip_engine_destroy(mip_engine *e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
+  if (e->stream3) (void)hipStreamSynchronize(e->stream3);
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables})
     if (p) (void)hipFree(p);
@@ -368,11 +374,15 @@ int mip_engine_destroy(mip_engine *e) {
   for (hipEvent_t ev : e->queue_done)
     if (ev) (void)hipEventDestroy(ev);
   if (e->refs_done) (void)hipEventDestroy(e->refs_done);
+  for (int i = 0; i < mip_engine::kHostSlots; i++)
+    for (hipEvent_t ev : {e->slot_up[i], e->slot_comp[i], e->slot_down[i]})
+      if (ev) (void)hipEventDestroy(ev);
   for (const mip_engine::Work &w : e->work)
     for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin})
       if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
+  if (e->stream3) (void)hipStreamDestroy(e->stream3);
   delete e;
   return 0;
 }
@@ -414,8 +424,12 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     if (_e != hipSuccess) return cleanup(fail("hipMalloc(%zu): %s", (size_t)(bytes), hipGetErrorString(_e))); \
   } while (0)
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail("hipStreamCreate failed"));
+  for (int i = 0; i < mip_engine::kHostSlots; i++)
+    for (hipEvent_t *ev : {&e->slot_up[i], &e->slot_comp[i], &e->slot_down[i]})
+      if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   ALLOC(e->d_frames, fs * nb * 2);
   if (o.filter != MIP_FILTER_NONE) ALLOC(e->d_refs, fs * nb * 2);
   ALLOC(e->d_costs, ncost * 4);
@@ -596,28 +610,36 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
   if (wait_refs_readers(e) != 0) return -1;
   const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
   // Chunks of `sb` frames rotate over `nslots` slots of the engine buffers (a quarter or a
-  // half of max_batch each) and alternate between two streams (H2D, [filter], search, D2H
-  // in order on each), so one chunk's transfers overlap the neighbouring chunks' searches
-  // and H2D / D2H run on both copy engines at once.  A slot is reused nslots chunks later,
-  // on the same stream (nslots is even), so stream order protects it.  Transfers run at DMA
-  // rate from page-locked host memory (mip_host_alloc); pageable buffers are staged by the
-  // runtime.
+  // half of max_batch each) through a three-stream pipeline: stream2 uploads chunk k+1 while
+  // `stream` searches chunk k and stream3 downloads chunk k-1, so the copy engines (H2D and
+  // D2H) and the compute run concurrently and the search kernels keep the whole GPU.  Per
+  // slot: the upload waits until the previous chunk of the slot has been searched (its
+  // frames / refs are free), the search waits for the upload and for the previous download
+  // of the slot's outputs, the download waits for the search.  Transfers run at DMA rate
+  // from page-locked host memory (mip_host_alloc); pageable buffers are staged by the runtime.
   const int nslots = e->opts.max_batch >= 16 ? 4 : (e->opts.max_batch >= 2 ? 2 : 1);
   const int sb = e->opts.max_batch / nslots;
+  const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
+  const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
   for (int f0 = 0, k = 0; f0 < nframes; f0 += sb, k++) {
     const int nb = std::min(sb, nframes - f0);
-    const int h = nslots > 1 ? (k & 1) : 0;
-    const hipStream_t st = h ? e->stream2 : e->stream;
-    const size_t fo = (size_t)(k % nslots) * sb;  // first engine frame slot of this chunk
+    const int sl = k % nslots;
+    const bool reuse = k >= nslots;  // the slot served chunk k - nslots in this call
+    const size_t fo = (size_t)sl * sb;  // first engine frame slot of this chunk
     uint16_t *d_frames = e->d_frames + fo * fs;
-    HIP_TRY(hipMemcpyAsync(d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, st));
+    if (reuse) HIP_TRY(hipStreamWaitEvent(up, e->slot_comp[sl], 0));
+    HIP_TRY(hipMemcpyAsync(d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, up));
     const uint16_t *d_refs = nullptr;
     if (refs_or_null) {
-      HIP_TRY(hipMemcpyAsync(e->d_refs + fo * fs, refs_or_null + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(e->d_refs + fo * fs, refs_or_null + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, up));
       d_refs = e->d_refs + fo * fs;
-    } else if (e->opts.filter != MIP_FILTER_NONE) {
+    }
+    HIP_TRY(hipEventRecord(e->slot_up[sl], up));
+    HIP_TRY(hipStreamWaitEvent(comp, e->slot_up[sl], 0));
+    if (reuse && any_out) HIP_TRY(hipStreamWaitEvent(comp, e->slot_down[sl], 0));
+    if (!refs_or_null && e->opts.filter != MIP_FILTER_NONE) {
       if (mip_filter_device(d_frames, e->d_refs + fo * fs, e->width, e->height, nb, e->opts.filter,
-                            e->opts.kernel_idx, st) != 0)
+                            e->opts.kernel_idx, comp) != 0)
         return -1;
       d_refs = e->d_refs + fo * fs;
     }
@@ -625,17 +647,22 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
     int32_t *d_sad = sad_out ? e->d_sad + fo * cpf : nullptr, *d_satd = satd_out ? e->d_satd + fo * cpf : nullptr;
     uint8_t *d_best = best_mode_out ? e->d_best + fo * upf : nullptr;
     int32_t *d_best_cost = best_cost_out ? e->d_best_cost + fo * upf : nullptr;
-    if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, st) != 0)
+    if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp) != 0)
       return -1;
-    if (costs_out) HIP_TRY(hipMemcpyAsync(costs_out + f0 * cpf, d_costs, nb * cpf * 4, hipMemcpyDeviceToHost, st));
-    if (sad_out) HIP_TRY(hipMemcpyAsync(sad_out + f0 * cpf, d_sad, nb * cpf * 4, hipMemcpyDeviceToHost, st));
-    if (satd_out) HIP_TRY(hipMemcpyAsync(satd_out + f0 * cpf, d_satd, nb * cpf * 4, hipMemcpyDeviceToHost, st));
-    if (best_mode_out) HIP_TRY(hipMemcpyAsync(best_mode_out + f0 * upf, d_best, nb * upf, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
+    if (!any_out) continue;
+    HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));
+    if (costs_out) HIP_TRY(hipMemcpyAsync(costs_out + f0 * cpf, d_costs, nb * cpf * 4, hipMemcpyDeviceToHost, down));
+    if (sad_out) HIP_TRY(hipMemcpyAsync(sad_out + f0 * cpf, d_sad, nb * cpf * 4, hipMemcpyDeviceToHost, down));
+    if (satd_out) HIP_TRY(hipMemcpyAsync(satd_out + f0 * cpf, d_satd, nb * cpf * 4, hipMemcpyDeviceToHost, down));
+    if (best_mode_out) HIP_TRY(hipMemcpyAsync(best_mode_out + f0 * upf, d_best, nb * upf, hipMemcpyDeviceToHost, down));
     if (best_cost_out)
-      HIP_TRY(hipMemcpyAsync(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, hipMemcpyDeviceToHost, down));
+    HIP_TRY(hipEventRecord(e->slot_down[sl], down));
   }
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream2));
+  HIP_TRY(hipStreamSynchronize(up));
+  HIP_TRY(hipStreamSynchronize(comp));
+  HIP_TRY(hipStreamSynchronize(down));
   e->refs_pending = false;
   return 0;
 }
