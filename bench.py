@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- 1080p frames/s of the full MIP mode search over all 47 CU shapes.
 
-One *step* = one pass of the fused HIP search over a batch of B (default 32) synthetic
+One *step* = one pass of the fused HIP search over a batch of B (default 128) synthetic
 1920x1080 frames resident in HBM (original references, BASELINE.json configs[1]), writing the complete
 int32 cost table (97840 entries per CTU, the reference's minSadHad table).  Frames shard
 across GPUs (one process per GPU, no data-path collective; RCCL only carries the barrier
@@ -16,9 +16,13 @@ Rank 0 prints one JSON line (contract in the task statement), plus:
                 the kernel runs on, and the PMC-measured traffic when profiles/ holds it;
   valu          the bound that actually applies to this path: VALU instruction issue.
                 Wave64 VALU instructions per launch (PMC SQ_INSTS_VALU, profiles/traffic.json)
-                over the live launch time against the chip's issue rate (1024 SIMDs x one
-                wave64 instruction per 4 cycles at 2.4 GHz), plus the measured issue
-                utilization; the SURVEY 8d algorithmic op count is reported alongside;
+                over the live launch time against the single-issue rate (1024 SIMDs x one
+                wave64 instruction per quad-cycle at 2.4 GHz), the PMC issue rate per SIMD
+                quad-cycle and its dual-issued share (SQ_ACTIVE_INST_VALU2).  gfx950 issues a
+                second VALU instruction in the same quad-cycle only for simple VOP1/VOP2 forms
+                from another wave; measured ceilings (profiles/r02_dual_census.txt, 4 waves per
+                SIMD): 1.37 per quad-cycle for an all-eligible stream, 0.86 for a stream of none;
+                the SURVEY 8d algorithmic op count is reported alongside;
   filter        the alternative-reference low-pass filter of BASELINE configs[2]
                 (filterFrame_2d_float_5x5_quarterCtu, KernelIdx 2) on the same frames:
                 HBM roofline (one frame read + one write per frame) and the alt-refs
@@ -42,9 +46,13 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 METRIC = "1080p frames/sec, full MIP mode search over all CU sizes; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E peak (spec)
 MFMA_F16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md, dense f16/bf16 matrix peak
-# VALU issue: 256 CUs x 4 SIMDs, one wave64 instruction per 4 cycles each, 2.4 GHz
-# (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s.
+# VALU issue: 256 CUs x 4 SIMDs, one wave64 instruction per quad-cycle (4 clocks) each, 2.4 GHz
+# (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s.  Dual issue (two eligible instructions
+# in one quad-cycle) raises it for simple VOP1/VOP2 forms only: measured ceilings per SIMD
+# quad-cycle at 4 waves/SIMD (tools/dual_census.sh, profiles/r02_dual_census.txt).
 VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
+DUAL_CEILINGS = {"all_dual_eligible": 1.37, "none_dual_eligible": 0.86, "unit": "VALU instructions per SIMD quad-cycle",
+                 "source": "profiles/r02_dual_census.txt (4 waves/SIMD)"}
 # SURVEY.md section 8d algorithmic op model per CTU: GEMV 40.4 M MAC (on MFMA here) and
 # 99.6 M vector ops (upsampling 13.8 + 19.9 M, SAD 19.3 M, SATD 46.6 M) -- the VALU share.
 VECTOR_OPS_PER_CTU = 99.6e6
@@ -94,6 +102,9 @@ def valu_section(pmc, kernel_ms, alg_ops):
     out = {"bound": "valu-issue", "unit": "G wave64 VALU instructions/s", "peak": round(VALU_PEAK_INSTS / 1e9, 1),
            "achieved": None, "frac": None, "valu_insts_per_launch": insts,
            "issue_utilization": pmc.get("valu_issue_utilization"),
+           "issue_per_simd_quad_cycle": pmc.get("valu_insts_per_simd_quad_cycle"),
+           "dual_issue_share": pmc.get("valu_dual_issue_share"),
+           "issue_ceilings": DUAL_CEILINGS,
            "algorithmic_vector_ops_per_s": round(alg_ops / (kernel_ms * 1e-3) / 1e12, 2),
            "algorithmic_unit": "T int ops/s (SURVEY 8d model, 99.6 M vector ops per CTU)"}
     if insts:
@@ -192,7 +203,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames-per-step", type=int, default=32)
+    ap.add_argument("--frames-per-step", type=int, default=128)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x1080)

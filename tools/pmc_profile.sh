@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out}/pmc
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:-"--frames-per-step 32 --steps 3 --warmup 1 --no-cpu-baseline --no-reference-gpu --no-latency --no-end-to-end"}
+ARGS=${BENCH_ARGS:-"--frames-per-step 128 --steps 3 --warmup 1 --no-cpu-baseline --no-reference-gpu --no-latency --no-end-to-end"}
 i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
@@ -19,5 +19,6 @@ SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST
 FETCH_SIZE
 WRITE_SIZE
 SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE
+SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE
 LIST
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"

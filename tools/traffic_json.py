@@ -13,7 +13,7 @@ import sys
 
 root, key, out = sys.argv[1], sys.argv[2], sys.argv[3]
 COUNTERS = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
-            "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16")
+            "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_ACTIVE_INST_VALU2")
 SEARCH = "mip_search_kernel<false>"          # original-reference search (the bench `value`)
 FILTER = "filter_kernel<2, true, false>"    # BASELINE configs[2] filter (bench `filter`)
 
@@ -48,12 +48,17 @@ def traffic(vals):
 s_vals = collect(SEARCH)
 rec = traffic(s_vals) or {}
 valu, grbm = mean(s_vals, "SQ_INSTS_VALU"), mean(s_vals, "GRBM_GUI_ACTIVE")
-# GRBM_GUI_ACTIVE is summed over the 8 XCDs; a wave64 VALU instruction issues in 4 cycles on
-# one of the 1024 SIMDs (MI355X_MICROARCH.md).
+# GRBM_GUI_ACTIVE is summed over the 8 XCDs.  A SIMD issues one VALU instruction per
+# quad-cycle (4 clocks), or two when both are dual-issue eligible (simple VOP1/VOP2 forms
+# from two waves, SQ_ACTIVE_INST_VALU2; tools/dual_census.sh): issue rate = VALU
+# instructions per SIMD quad-cycle over the 1024 SIMDs.
 util = valu * 4 / (1024 * grbm / 8) if valu and grbm else None
+dual = mean(s_vals, "SQ_ACTIVE_INST_VALU2")
 conf, lds = mean(s_vals, "SQ_LDS_BANK_CONFLICT"), mean(s_vals, "SQ_LDS_IDX_ACTIVE")
 rec.update({"kernel": SEARCH, "valu_insts_per_launch": valu, "gui_active_cycles_per_xcd": grbm and grbm / 8,
             "valu_issue_utilization": util and round(util, 4),
+            "valu_insts_per_simd_quad_cycle": util and round(util, 4),
+            "valu_dual_issue_share": dual and valu and round(dual / valu, 4),
             "lds_bank_conflict_frac": conf and lds and round(conf / lds, 4),
             "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/pmc_profile.sh); "
                       "FETCH_SIZE KiB x1024 x2 (gfx950 correction), WRITE_SIZE KiB x1024"})
