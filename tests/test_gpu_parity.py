@@ -305,3 +305,21 @@ def test_engine_filter_scratch_shared_by_two_streams(gpu_available):
         for sel, c in outs:
             assert np.array_equal(c.cpu().numpy(), want[sel])
         assert np.array_equal(mid, want[2:4])
+
+
+def test_host_pipeline_decisions_only_with_caller_refs(gpu_available):
+    """mip_search_frames with two buffer slots (max_batch 4: chunks of 2 frames), caller
+    references uploaded through the pipeline next to the frames, 7 frames (slots reused,
+    uneven last chunk) and decisions only (no cost-table download): each slot's upload must
+    wait for the previous search of that slot, each search for its upload."""
+    w, h, n = 256, 136, 7
+    frames = synth_frames(w, h, n, 0x7D1, 0)
+    refs = synth_frames(w, h, n, 0x7D2, 0)
+    with MipEngine(w, h, max_batch=4) as eng:
+        out = eng.search(frames, refs=refs, costs=False, best=True)
+    assert "cost" not in out
+    nct = layout.num_ctus(w, h)
+    for f in range(n):
+        bm, bc = layout.best_modes(O.search(frames[f], refs[f]), nct)
+        assert np.array_equal(out["best_mode"][f], bm), f
+        assert np.array_equal(out["best_cost"][f], bc), f

@@ -81,8 +81,8 @@ constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 16;    // > every uniform B off
 constexpr int kUnavailable = 0x7fffffff;
 
 // Biased residuals.  The Hadamard butterflies of the SATD run as plain 32-bit adds /
-// subtracts on both 16-bit halves at once (v_add_u32 / v_sub_u32 issue at twice the rate
-// of the packed v_pk_* ops on gfx950, tools/valu_rate.hip), which is exact only while no
+// subtracts on both 16-bit halves at once (v_add_u32 / v_sub_u32 can be dual-issued on
+// gfx950, the packed v_pk_* ops cannot: tools/dual_census.sh), which is exact only while no
 // half ever goes negative or past 65535.  So every value carries a bias: the original
 // samples are staged into LDS as o + kBiasD[y & 1][x & 3] (the 4x4 block position), so the
 // residual o - p arrives biased, and the biases propagate through the butterflies to
