@@ -88,8 +88,9 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
                       int kernel_idx, uint16_t *out);
 
 /* Full MIP search of `nframes` host frames: H2D, [filter], search, D2H, in chunks of
- * max_batch/4 (max_batch >= 16) or max_batch/2 frames over two streams, so that each
- * chunk's transfers overlap the neighbouring chunks' searches.
+ * max_batch/4 (max_batch >= 16) or max_batch/2 frames through the engine's three streams
+ * (uploads, search, downloads), so that one chunk's upload, the previous chunk's search and
+ * the one before's download run at the same time.
  * Replaces the per-frame loop main.cpp:678-1241 + readMemobjsIntoArray_Distortion.
  * refs_or_null: caller-provided reference-sample frames (alternative samples computed
  * elsewhere); NULL = originals, or the engine's filter when opts.filter != NONE.
