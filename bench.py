@@ -265,8 +265,12 @@ def main():
     max_kernel_ms = dist_max(kernel_ms, world, dev)
     value, ms_per_step = aggregate(B, args.steps, world, max_elapsed)
 
-    refs_desc = ("original references (BASELINE configs[1])" if args.refs_filter is None else
+    cfg = {(1920, 1080, None): 1, (1920, 1080, "filterFrame_2d_float_5x5_quarterCtu"): 2, (3840, 2160, None): 3,
+           (7680, 4320, "filterFrame_2d_int_quarterCtu"): 4}.get((W, H, args.refs_filter))
+    refs_desc = ("original references" if args.refs_filter is None else
                  "alternative references %s KernelIdx %d filtered inside the step" % (args.refs_filter, args.kernel_idx))
+    if cfg is not None:
+        refs_desc += " (BASELINE configs[%d])" % cfg
     if rank == 0:
         alg_bytes = algorithmic_bytes_per_frame(W, H) * B
         achieved = alg_bytes / (max_kernel_ms * 1e-3) / 1e9
