@@ -103,6 +103,20 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
                       int nframes, int32_t *costs_out, uint8_t *best_mode_out,
                       int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out);
 
+/* mip_search_frames without the final wait: enqueues the call's chunks behind the calls
+ * still in flight (the upload / search / download pipeline stays full from one call to the
+ * next) and returns a ticket (> 0) in *ticket.  The host buffers must stay valid and
+ * unmodified (inputs) / unread (outputs) until mip_wait(e, ticket) returns.  Calls complete
+ * in order.  mip_filter_frames waits for every call in flight. */
+int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
+                            int nframes, int32_t *costs_out, uint8_t *best_mode_out,
+                            int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out,
+                            uint64_t *ticket);
+
+/* Block until the call with this ticket (and every earlier one) has completed: its outputs
+ * are in host memory. */
+int mip_wait(mip_engine *e, uint64_t ticket);
+
 /* Device-resident variant (inputs already in HBM; all pointers are device pointers,
  * `stream` is a hipStream_t; NULL means the default (null) stream, as in HIP).
  * Asynchronous on `stream`.

@@ -323,3 +323,56 @@ def test_host_pipeline_decisions_only_with_caller_refs(gpu_available):
         bm, bc = layout.best_modes(O.search(frames[f], refs[f]), nct)
         assert np.array_equal(out["best_mode"][f], bm), f
         assert np.array_equal(out["best_cost"][f], bc), f
+
+
+def test_async_host_calls_in_flight(gpu_available):
+    """mip_search_frames_async: four calls queued back to back (different frames, outputs
+    and reference sources; slots reused across calls) complete in order with the oracle's
+    tables; waiting for an earlier ticket after a later one is a no-op; unknown tickets are
+    errors."""
+    w, h = 256, 136
+    frames = synth_frames(w, h, 9, 0xA51, 0)
+    refs = synth_frames(w, h, 3, 0xA52, 0)
+    nct = layout.num_ctus(w, h)
+    with MipEngine(w, h, max_batch=4) as eng:
+        t1 = eng.search_async(frames[0:3], best=True)
+        t2 = eng.search_async(frames[3:5], costs=False, best=True)
+        t3 = eng.search_async(frames[5:8], refs=refs)
+        t4 = eng.search_async(frames[8:9])
+        o4 = eng.wait(t4)
+        o1, o2, o3 = eng.wait(t1), eng.wait(t2), eng.wait(t3)
+        with pytest.raises(MipError):
+            eng.wait(type(t4)(t4.value + 1, {}, None))
+    for f in range(3):
+        oc = O.search(frames[f])
+        assert np.array_equal(o1["cost"][f], oc), f
+        assert np.array_equal(o1["best_mode"][f], layout.best_modes(oc, nct)[0]), f
+    for f in range(2):
+        bm, bc = layout.best_modes(O.search(frames[3 + f]), nct)
+        assert np.array_equal(o2["best_mode"][f], bm) and np.array_equal(o2["best_cost"][f], bc), f
+    for f in range(3):
+        assert np.array_equal(o3["cost"][f], O.search(frames[5 + f], refs[f])), f
+    assert np.array_equal(o4["cost"][0], O.search(frames[8]))
+
+
+def test_async_host_calls_and_device_filter_scratch(gpu_available):
+    """An engine with a filter: asynchronous host calls (filtering into the reference
+    scratch per slot) in flight while a device-API search filters into the same scratch on
+    another stream -- the device search waits for the host pipeline, every table matches."""
+    import torch
+    filt, k = "filterFrame_2d_int_quarterCtu", 1
+    w, h = 264, 136
+    frames = synth_frames(w, h, 6, 0xA61, 0)
+    want = np.stack([O.search(frames[f], O.filter_frame(frames[f], filt, k)) for f in range(6)])
+    d = torch.from_numpy(frames[4:6].astype(np.int16)).cuda()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    with MipEngine(w, h, max_batch=2, filter=filt, kernel_idx=k) as eng:
+        t1 = eng.search_async(frames[0:2])
+        t2 = eng.search_async(frames[2:4])
+        dc = eng.search_device(d, stream=s)
+        o1, o2 = eng.wait(t1), eng.wait(t2)
+        torch.cuda.synchronize()
+        assert np.array_equal(dc.cpu().numpy(), want[4:6])
+    assert np.array_equal(o1["cost"], want[0:2])
+    assert np.array_equal(o2["cost"], want[2:4])

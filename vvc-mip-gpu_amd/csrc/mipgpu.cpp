@@ -259,6 +259,16 @@ struct mip_engine {
   hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
   static constexpr int kHostSlots = 4;
   hipEvent_t slot_up[kHostSlots] = {}, slot_comp[kHostSlots] = {}, slot_down[kHostSlots] = {};
+  // Chunks run through the slots in one global sequence across host-API calls, so that
+  // asynchronous calls (mip_search_frames_async) keep the pipeline full; call k completes
+  // at call_done[(k - 1) % kCallRing] (tickets are 1-based call numbers).
+  uint64_t host_chunks = 0, host_calls = 0;
+  static constexpr int kCallRing = 64;
+  hipEvent_t call_done[kCallRing] = {};
+  // Last host-API search (stream `stream`): device-API searches that filter into the
+  // engine's reference scratch wait for it (the host pipeline uses the same buffer).
+  hipEvent_t host_done = nullptr;
+  bool host_pending = false;
   uint16_t *d_frames = nullptr, *d_refs = nullptr;
   int32_t *d_costs = nullptr, *d_sad = nullptr, *d_satd = nullptr, *d_best_cost = nullptr;
   uint8_t *d_best = nullptr;
@@ -377,6 +387,9 @@ int mip_engine_destroy(mip_engine *e) {
   for (int i = 0; i < mip_engine::kHostSlots; i++)
     for (hipEvent_t ev : {e->slot_up[i], e->slot_comp[i], e->slot_down[i]})
       if (ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->call_done)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->host_done) (void)hipEventDestroy(e->host_done);
   for (const mip_engine::Work &w : e->work)
     for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin})
       if (p) (void)hipFree(p);
@@ -430,6 +443,10 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   for (int i = 0; i < mip_engine::kHostSlots; i++)
     for (hipEvent_t *ev : {&e->slot_up[i], &e->slot_comp[i], &e->slot_down[i]})
       if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
+  for (hipEvent_t &ev : e->call_done)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
+  if (hipEventCreateWithFlags(&e->host_done, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail("hipEventCreate failed"));
   ALLOC(e->d_frames, fs * nb * 2);
   if (o.filter != MIP_FILTER_NONE) ALLOC(e->d_refs, fs * nb * 2);
   ALLOC(e->d_costs, ncost * 4);
@@ -514,6 +531,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   if (engine_refs) {
     if (nframes > e->opts.max_batch) return fail("nframes %d > max_batch %d", nframes, e->opts.max_batch);
     if (e->refs_pending) HIP_TRY(hipStreamWaitEvent(s, e->refs_done, 0));  // last reader of d_refs
+    if (e->host_pending) HIP_TRY(hipStreamWaitEvent(s, e->host_done, 0));  // host calls in flight
     if (mip_filter_device(d_frames, e->d_refs, e->width, e->height, nframes, e->opts.filter,
                           e->opts.kernel_idx, s) != 0)
       return -1;
@@ -598,16 +616,18 @@ int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d
                             (hipStream_t)stream);
 }
 
-int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
-                      int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
-                      int32_t *satd_out) {
-  if (!e || !frames || nframes < 1) return fail("bad search arguments");
+int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
+                            int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
+                            int32_t *satd_out, uint64_t *ticket) {
+  if (!e || !frames || nframes < 1 || !ticket) return fail("bad search arguments");
+  *ticket = 0;
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
   HIP_TRY(hipSetDevice(e->device));
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
     HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
   if (wait_refs_readers(e) != 0) return -1;
+  e->refs_pending = false;  // the waits above order every later use of the engine streams
   const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
   // Chunks of `sb` frames rotate over `nslots` slots of the engine buffers (a quarter or a
   // half of max_batch each) through a three-stream pipeline: stream2 uploads chunk k+1 while
@@ -615,16 +635,19 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
   // D2H) and the compute run concurrently and the search kernels keep the whole GPU.  Per
   // slot: the upload waits until the previous chunk of the slot has been searched (its
   // frames / refs are free), the search waits for the upload and for the previous download
-  // of the slot's outputs, the download waits for the search.  Transfers run at DMA rate
-  // from page-locked host memory (mip_host_alloc); pageable buffers are staged by the runtime.
+  // of the slot's outputs, the download waits for the search.  The chunk sequence (and so
+  // the slot rotation and these waits) continues across calls, so asynchronous calls queue
+  // behind each other without draining the pipeline.  Transfers run at DMA rate from
+  // page-locked host memory (mip_host_alloc); pageable buffers are staged by the runtime.
   const int nslots = e->opts.max_batch >= 16 ? 4 : (e->opts.max_batch >= 2 ? 2 : 1);
   const int sb = e->opts.max_batch / nslots;
   const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
   const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
-  for (int f0 = 0, k = 0; f0 < nframes; f0 += sb, k++) {
+  for (int f0 = 0; f0 < nframes; f0 += sb) {
     const int nb = std::min(sb, nframes - f0);
-    const int sl = k % nslots;
-    const bool reuse = k >= nslots;  // the slot served chunk k - nslots in this call
+    const uint64_t k = e->host_chunks++;
+    const int sl = (int)(k % nslots);
+    const bool reuse = k >= (uint64_t)nslots;  // the slot served chunk k - nslots (this or an earlier call)
     const size_t fo = (size_t)sl * sb;  // first engine frame slot of this chunk
     uint16_t *d_frames = e->d_frames + fo * fs;
     if (reuse) HIP_TRY(hipStreamWaitEvent(up, e->slot_comp[sl], 0));
@@ -636,7 +659,7 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
     }
     HIP_TRY(hipEventRecord(e->slot_up[sl], up));
     HIP_TRY(hipStreamWaitEvent(comp, e->slot_up[sl], 0));
-    if (reuse && any_out) HIP_TRY(hipStreamWaitEvent(comp, e->slot_down[sl], 0));
+    if (reuse) HIP_TRY(hipStreamWaitEvent(comp, e->slot_down[sl], 0));
     if (!refs_or_null && e->opts.filter != MIP_FILTER_NONE) {
       if (mip_filter_device(d_frames, e->d_refs + fo * fs, e->width, e->height, nb, e->opts.filter,
                             e->opts.kernel_idx, comp) != 0)
@@ -660,11 +683,32 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
       HIP_TRY(hipMemcpyAsync(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, hipMemcpyDeviceToHost, down));
     HIP_TRY(hipEventRecord(e->slot_down[sl], down));
   }
-  HIP_TRY(hipStreamSynchronize(up));
-  HIP_TRY(hipStreamSynchronize(comp));
-  HIP_TRY(hipStreamSynchronize(down));
-  e->refs_pending = false;
+  HIP_TRY(hipEventRecord(e->host_done, comp));
+  e->host_pending = true;
+  const uint64_t call = ++e->host_calls;
+  HIP_TRY(hipEventRecord(e->call_done[(call - 1) % mip_engine::kCallRing], any_out ? down : comp));
+  *ticket = call;
   return 0;
+}
+
+int mip_wait(mip_engine *e, uint64_t ticket) {
+  if (!e) return fail("engine is NULL");
+  if (ticket == 0 || ticket > e->host_calls) return fail("unknown ticket %llu", (unsigned long long)ticket);
+  HIP_TRY(hipSetDevice(e->device));
+  // a ticket older than the ring shares its event with a later call: waiting for that one
+  // is later than needed, never too early
+  HIP_TRY(hipEventSynchronize(e->call_done[(ticket - 1) % mip_engine::kCallRing]));
+  return 0;
+}
+
+int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
+                      int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
+                      int32_t *satd_out) {
+  uint64_t ticket = 0;
+  if (mip_search_frames_async(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out, sad_out,
+                              satd_out, &ticket) != 0)
+    return -1;
+  return mip_wait(e, ticket);
 }
 
 int mip_host_alloc(size_t bytes, void **out) {
@@ -686,6 +730,10 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
   const size_t fs = (size_t)e->width * e->height;
   if (!e->d_refs) HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
   if (wait_refs_readers(e) != 0) return -1;
+  // asynchronous host searches still in flight use d_frames / d_refs: let them finish
+  HIP_TRY(hipStreamSynchronize(e->stream2));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream3));
   for (int f0 = 0; f0 < nframes; f0 += e->opts.max_batch) {
     const int nb = std::min(e->opts.max_batch, nframes - f0);
     HIP_TRY(hipMemcpyAsync(e->d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, e->stream));

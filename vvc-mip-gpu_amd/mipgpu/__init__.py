@@ -82,6 +82,8 @@ def library():
         "mip_cu_position": (ip, [ip, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]),
         "mip_filter_frames": (ip, [vp, vp, ip, ip, ip, vp]),
         "mip_search_frames": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp]),
+        "mip_search_frames_async": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
+        "mip_wait": (ip, [vp, ctypes.c_uint64]),
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
         "mip_topk_device": (ip, [vp, ip, ip, ip, ip, vp, vp, vp]),
@@ -122,6 +124,14 @@ def pinned_empty(shape, dtype) -> np.ndarray:
     buf = (ctypes.c_byte * max(1, count * dt.itemsize)).from_address(p.value)
     weakref.finalize(buf, library().mip_host_free, ctypes.c_void_p(p.value))
     return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
+
+
+class _Ticket:
+    """An asynchronous host search in flight: its number, its outputs, and its inputs (kept
+    alive until the search has completed)."""
+
+    def __init__(self, value, out, keep):
+        self.value, self.out, self._keep = value, out, keep
 
 
 class MipEngine:
@@ -181,8 +191,15 @@ class MipEngine:
     def search(self, frames, refs=None, costs=True, best=False, sad_satd=False, out=None):
         """Full MIP search of host frames ([F,H,W] or [H,W] uint16).  Returns a dict with
         'cost' [F, nCTUs*97840] int32 and optionally 'best_mode' / 'best_cost' [F, nCTUs*5380]
-        (decision lists [F, nCTUs*5380, K] when the engine has best_k = K > 1), 'sad' / 'satd'.  `out` may supply any of these arrays (e.g. from pinned_empty, for
-        DMA-rate transfers); the others are allocated."""
+        (decision lists [F, nCTUs*5380, K] when the engine has best_k = K > 1), 'sad' / 'satd'.
+        `out` may supply any of these arrays (e.g. from pinned_empty, for DMA-rate
+        transfers); the others are allocated."""
+        return self.wait(self.search_async(frames, refs, costs, best, sad_satd, out))
+
+    def search_async(self, frames, refs=None, costs=True, best=False, sad_satd=False, out=None):
+        """As search(), without waiting (mip_search_frames_async): the call queues behind
+        the calls in flight and returns a ticket; wait(ticket) returns the output dict.  The
+        ticket keeps the input and output arrays alive until then."""
         f = self._frames(frames)
         r = None if refs is None else self._frames(refs)
         n = f.shape[0]
@@ -199,19 +216,25 @@ class MipEngine:
                 raise MipError(f"out[{key!r}] must be a C-contiguous {np.dtype(dtype)} array of shape {shape}")
             return a
 
-        out = {}
-        cost = buf("cost", costs, self.costs_per_frame, np.int32)
+        res = {}
         bcols = self.cus_per_frame if self.best_k == 1 else (self.cus_per_frame, self.best_k)
-        bm = buf("best_mode", best, bcols, np.uint8)
-        bc = buf("best_cost", best, bcols, np.int32)
-        sad = buf("sad", sad_satd, self.costs_per_frame, np.int32)
-        satd = buf("satd", sad_satd, self.costs_per_frame, np.int32)
-        _check(library().mip_search_frames(self._h, _ptr(f), _ptr(r), n, _ptr(cost), _ptr(bm), _ptr(bc),
-                                           _ptr(sad), _ptr(satd)))
-        for k, v in (("cost", cost), ("best_mode", bm), ("best_cost", bc), ("sad", sad), ("satd", satd)):
-            if v is not None:
-                out[k] = v
-        return out
+        for key, want, cols, dt in (("cost", costs, self.costs_per_frame, np.int32),
+                                    ("best_mode", best, bcols, np.uint8), ("best_cost", best, bcols, np.int32),
+                                    ("sad", sad_satd, self.costs_per_frame, np.int32),
+                                    ("satd", sad_satd, self.costs_per_frame, np.int32)):
+            a = buf(key, want, cols, dt)
+            if a is not None:
+                res[key] = a
+        t = ctypes.c_uint64()
+        _check(library().mip_search_frames_async(self._h, _ptr(f), _ptr(r), n, _ptr(res.get("cost")),
+                                                 _ptr(res.get("best_mode")), _ptr(res.get("best_cost")),
+                                                 _ptr(res.get("sad")), _ptr(res.get("satd")), ctypes.byref(t)))
+        return _Ticket(t.value, res, (f, r))
+
+    def wait(self, ticket):
+        """Block until an asynchronous search has completed; returns its output dict."""
+        _check(library().mip_wait(self._h, ctypes.c_uint64(ticket.value)))
+        return ticket.out
 
     def filter_frames(self, frames, filter, kernel_idx=0):
         f = self._frames(frames)
