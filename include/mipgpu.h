@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MIPGPU_ABI_VERSION 3
+#define MIPGPU_ABI_VERSION 4
 #define MIP_COSTS_PER_CTU_ABI 97840
 #define MIP_CUS_PER_CTU_ABI 5380
 #define MIP_COST_UNAVAILABLE 0x7fffffff

@@ -685,8 +685,11 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
   }
   HIP_TRY(hipEventRecord(e->host_done, comp));
   e->host_pending = true;
+  // completion on the download stream, after this call's search and every earlier call's
+  // downloads: calls complete in order
+  if (!any_out) HIP_TRY(hipStreamWaitEvent(down, e->host_done, 0));
   const uint64_t call = ++e->host_calls;
-  HIP_TRY(hipEventRecord(e->call_done[(call - 1) % mip_engine::kCallRing], any_out ? down : comp));
+  HIP_TRY(hipEventRecord(e->call_done[(call - 1) % mip_engine::kCallRing], down));
   *ticket = call;
   return 0;
 }
