@@ -126,6 +126,17 @@ int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d
                       int nframes, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
                       uint8_t *d_best_mode, int32_t *d_best_cost, void *stream);
 
+/* mip_search_device restricted to the CTUs [ctu_begin, ctu_end) (raster order) of every
+ * frame: writes exactly those CTUs' blocks of the full-size cost / SAD / SATD tables and
+ * leaves the others untouched.  The frames are complete (CUs at the range's top and left
+ * edge read their reference samples from the rows / columns outside the range, the filter
+ * runs over whole frames), so ranges that tile the frame give the full table: one large
+ * frame split into CTU-row bands over several GPUs.  No decision
+ * lists (run mip_topk_device on the assembled table). */
+int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
+                            int nframes, int ctu_begin, int ctu_end, int32_t *d_costs,
+                            int32_t *d_sad, int32_t *d_satd, void *stream);
+
 /* Per-CU decision lists (no reference counterpart; what an encoder's full-RD stage takes
  * from the cost table, e.g. VTM's numModesForFullRD MIP candidates): for every CU of
  * `nframes` device cost tables (reference layout), the k lowest-cost modes in increasing

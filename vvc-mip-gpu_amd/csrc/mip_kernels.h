@@ -59,10 +59,12 @@ struct SearchArgs {
   const uint4 *tables;    // kTableBytes: MIP matrices for the MFMA, see below
   int width, height;
   int ctu_cols, nctus;
+  int ctu0, nrange;       // CTUs searched: [ctu0, ctu0 + nrange) of every frame (whole frame:
+                          // 0, nctus); cost entries of the other CTUs are not written
   int slices;             // workgroups (task lists) per CTU quadrant
   uint32_t *queue;        // item counter pair {next item, workgroups done}, zero at launch;
                           // the kernel leaves it zero again
-  uint32_t nitems;        // frames * nctus * 4 * slices (set by launch_search)
+  uint32_t nitems;        // frames * nrange * 4 * slices (set by launch_search)
   uint64_t *wave_clock;   // profiling (MIPGPU_WAVE_TIMING): [workgroup][kClockSlots] cycles per
                           // task of the workgroup's list; else null
 };

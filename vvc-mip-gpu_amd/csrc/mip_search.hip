@@ -831,7 +831,7 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     __syncthreads();
     const uint32_t item = *cur_item;
     if (item >= a.nitems) break;  // workgroup-uniform
-    const int gx = item % per_ctu, ctu = (item / per_ctu) % a.nctus, frame = item / (per_ctu * a.nctus);
+    const int gx = item % per_ctu, ctu = a.ctu0 + (item / per_ctu) % a.nrange, frame = item / (per_ctu * a.nrange);
     const int slice = gx % a.slices, quad = gx / a.slices;
     const int ctu_x = 128 * (ctu % a.ctu_cols), ctu_y = 128 * (ctu / a.ctu_cols);
     const int fx0 = ctu_x + 64 * (quad & 1), fy0 = ctu_y + 64 * (quad >> 1);
@@ -971,7 +971,8 @@ int search_resident_groups(bool alt) {
 hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, hipStream_t s) {
   if (args.slices < 1 || !args.queue || resident < 1) return hipErrorInvalidValue;
   SearchArgs a = args;
-  a.nitems = (uint32_t)(4 * a.slices) * a.nctus * nframes;
+  if (a.ctu0 < 0 || a.nrange < 1 || a.ctu0 + a.nrange > a.nctus) return hipErrorInvalidValue;
+  a.nitems = (uint32_t)(4 * a.slices) * a.nrange * nframes;
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const size_t lds = search_lds_bytes(alt_refs);

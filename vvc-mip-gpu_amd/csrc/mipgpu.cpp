@@ -308,8 +308,8 @@ constexpr long long kMaxCus = (1LL << 31) - 256;
 // Slice count for a launch of `nframes`: items (quadrant x slice) for the persistent grid of
 // 512 workgroups.  Measured on MI355X at 1080p: 1 frame -> 2 slices 5076 frames/s (1: 4842,
 // 4: 4770), >= 2 frames -> 1 slice (2 frames: 5830 vs 5087 with 2 slices).
-const mip_engine::Work &pick_work(const mip_engine *e, int nframes) {
-  const long long wg1 = 4LL * e->nctus * nframes;  // workgroups at one slice
+const mip_engine::Work &pick_work(const mip_engine *e, int nframes, int nrange) {
+  const long long wg1 = 4LL * nrange * nframes;  // workgroups at one slice
   const int want = wg1 < 1000 ? 2 : 1;
   const mip_engine::Work *best = &e->work[0];
   for (const mip_engine::Work &w : e->work)
@@ -522,8 +522,11 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
 
 static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
-                              int32_t *d_best_cost, hipStream_t s) {
+                              int32_t *d_best_cost, hipStream_t s, int ctu0 = 0, int nrange = -1) {
   if (!e || !d_frames || !d_costs || nframes < 1) return fail("bad search arguments");
+  if (nrange < 0) nrange = e->nctus - ctu0;
+  if (ctu0 < 0 || nrange < 1 || ctu0 + nrange > e->nctus)
+    return fail("CTU range [%d, %d) outside the frame's %d CTUs", ctu0, ctu0 + nrange, e->nctus);
   const long long total_cus = (long long)nframes * e->nctus * MIP_CUS_PER_CTU;
   if (total_cus > kMaxCus) return fail("%d frames x %d CTUs exceed %lld CUs per launch", nframes, e->nctus, kMaxCus);
   const uint16_t *refs = d_refs;
@@ -544,7 +547,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.cost = d_costs;
   a.sad = d_sad;
   a.satd = d_satd;
-  const mip_engine::Work &work = pick_work(e, nframes);
+  const mip_engine::Work &work = pick_work(e, nframes, nrange);
   a.tasks = work.d_tasks;
   a.jobs = work.d_jobs;
   a.list_begin = work.d_lists;
@@ -555,6 +558,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.height = e->height;
   a.ctu_cols = e->ctu_cols;
   a.nctus = e->nctus;
+  a.ctu0 = ctu0;
+  a.nrange = nrange;
   a.slices = work.slices;
   // MIPGPU_WAVE_TIMING=file (profiling): per-task cycles appended to `file` (synchronous;
   // one binary record of uint64 [workgroup][wave][kClockSlots] per launch), and the task
@@ -562,7 +567,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   static const char *timing = getenv("MIPGPU_WAVE_TIMING");
   std::vector<uint64_t> clocks;
   if (timing) {
-    const size_t n = (size_t)4 * work.slices * e->nctus * nframes * mipgpu::kClockSlots;
+    const size_t n = (size_t)4 * work.slices * nrange * nframes * mipgpu::kClockSlots;
     HIP_TRY(hipMalloc((void **)&a.wave_clock, n * 8));
     HIP_TRY(hipMemsetAsync(a.wave_clock, 0, n * 8, s));
     clocks.resize(n);
@@ -614,6 +619,15 @@ int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, d_best_mode, d_best_cost,
                             (hipStream_t)stream);
+}
+
+int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
+                            int ctu_begin, int ctu_end, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
+                            void *stream) {
+  if (!e) return fail("engine is NULL");
+  HIP_TRY(hipSetDevice(e->device));
+  return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, nullptr, nullptr,
+                            (hipStream_t)stream, ctu_begin, ctu_end - ctu_begin);
 }
 
 int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,

@@ -85,6 +85,7 @@ def library():
         "mip_search_frames_async": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "mip_wait": (ip, [vp, ctypes.c_uint64]),
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
+        "mip_search_device_range": (ip, [vp, vp, vp, ip, ip, ip, vp, vp, vp, vp]),
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
         "mip_topk_device": (ip, [vp, ip, ip, ip, ip, vp, vp, vp]),
         "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
@@ -256,6 +257,16 @@ class MipEngine:
         _check(library().mip_search_device(self._h, _ptr(frames), _ptr(refs), n, _ptr(costs), _ptr(sad),
                                            _ptr(satd), _ptr(best_mode), _ptr(best_cost),
                                            ctypes.c_void_p(s.cuda_stream)))
+        return costs
+
+    def search_device_range(self, frames, ctu_begin, ctu_end, costs, refs=None, sad=None, satd=None, stream=None):
+        """search_device over the CTUs [ctu_begin, ctu_end) of every frame only
+        (mip_search_device_range): their blocks of the full-size `costs` are written."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device)
+        _check(library().mip_search_device_range(self._h, _ptr(frames), _ptr(refs), frames.shape[0], int(ctu_begin),
+                                                 int(ctu_end), _ptr(costs), _ptr(sad), _ptr(satd),
+                                                 ctypes.c_void_p(s.cuda_stream)))
         return costs
 
     def time_search_device(self, frames, costs, refs=None, reps=10) -> float:
