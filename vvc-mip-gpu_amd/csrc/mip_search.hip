@@ -60,6 +60,15 @@ constexpr ShapeStarts make_shape_starts() {
 static_assert(make_shape_starts().v[MIP_NUM_SHAPES] == MIP_CUS_PER_CTU, "shape table");
 __constant__ ShapeStarts c_shape_start = make_shape_starts();
 
+#ifndef MIP_PREFETCH
+#define MIP_PREFETCH 1  // next item's window loaded by the item's first idle wave (A/B knob)
+#endif
+#ifndef MIP_PF_BATCH
+#define MIP_PF_BATCH 6  // window loads in flight per lane in the prefetching wave
+#endif
+#ifndef MIP_WIN_UNROLL
+#define MIP_WIN_UNROLL 2  // windows of the vertical pass per loop iteration (A/B knob)
+#endif
 #ifndef MIP_ONLY_CLASS
 #define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
 #endif
@@ -524,8 +533,11 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
     // is walked incrementally, n_o = n_{o-1} + delta, with delta the exact 32-bit
     // difference of the packed pairs (see anchor_row); o = UV gives the anchor itself.
     constexpr int NB = G::UV / 4;  // blocks per window
-#pragma unroll 1
-    for (int k = k0; k < k1; k++) {
+    constexpr int NW = G::CHUNKED ? 4 : G::KV;  // windows in [k0, k1)
+    (void)k1;
+#pragma unroll MIP_WIN_UNROLL
+    for (int kk = 0; kk < NW; kk++) {
+      const int k = k0 + kk;
       s2 next[4];
       anchor_row<W, H>(red, k, x0, next);
       uint32_t delta[4], num[4];
@@ -765,22 +777,48 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
 // Stage the quadrant window (rows -1..63, columns -4..63) of one frame into LDS, each
 // sample plus its residual bias (kBiasD).  Samples outside the frame read as 0 (+ bias);
 // they only feed CUs whose results are discarded or padding branches that never select them.
+constexpr int kTileChunks = kPitch / 4;            // 17 chunks of 4 samples per row
+constexpr int kTileLoads = 65 * kTileChunks;       // 1105 8-byte chunks per quadrant window
+
+__device__ __forceinline__ uint2 tile_load(const uint16_t *frame, int width, int height, int x0, int y0, int i) {
+  const int row = i / kTileChunks, ch = i - row * kTileChunks;
+  const int fy = y0 - 1 + row, fx = x0 - kColOff + 4 * ch;
+  uint2 v = make_uint2(0, 0);
+  if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
+    v = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
+  return v;
+}
+
+__device__ __forceinline__ void tile_store(uint16_t *dst, int i, uint2 v) {
+  const int row = i / kTileChunks, ch = i - row * kTileChunks;
+  // residual bias of the sample's 4x4-block position (quadrant y = row - 1, x = 4ch - 4)
+  const uint32_t odd = (row - 1) & 1;
+  v.x += odd ? bias_word(1, 0) : bias_word(0, 0);
+  v.y += odd ? bias_word(1, 2) : bias_word(0, 2);
+  *reinterpret_cast<uint2 *>(dst + row * kPitch + 4 * ch) = v;
+}
+
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
                                            int x0, int y0) {
-  constexpr int kChunks = kPitch / 4;  // 17 chunks of 4 samples per row
-  for (int i = threadIdx.x; i < 65 * kChunks; i += blockDim.x) {
-    const int row = i / kChunks, ch = i - row * kChunks;
-    const int fy = y0 - 1 + row, fx = x0 - kColOff + 4 * ch;
-    uint2 v = make_uint2(0, 0);
-    if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
-      v = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
-    // residual bias of the sample's 4x4-block position (quadrant y = row - 1, x = 4ch - 4)
-    const uint32_t odd = (row - 1) & 1;
-    v.x += odd ? bias_word(1, 0) : bias_word(0, 0);
-    v.y += odd ? bias_word(1, 2) : bias_word(0, 2);
-    *reinterpret_cast<uint2 *>(dst + row * kPitch + 4 * ch) = v;
-  }
+  for (int i = threadIdx.x; i < kTileLoads; i += blockDim.x) tile_store(dst, i, tile_load(frame, width, height, x0, y0, i));
 }
+
+// Item = (frame, CTU, quadrant, slice) -> quadrant origin in the frame and frame index.
+struct ItemPos {
+  int frame, ctu, slice, quad, ctu_x, ctu_y, fx0, fy0;
+  __device__ __forceinline__ ItemPos(const SearchArgs &a, uint32_t item) {
+    const int per_ctu = 4 * a.slices;
+    const int gx = item % per_ctu;
+    ctu = a.ctu0 + (item / per_ctu) % a.nrange;
+    frame = item / (per_ctu * a.nrange);
+    slice = gx % a.slices;
+    quad = gx / a.slices;
+    ctu_x = 128 * (ctu % a.ctu_cols);
+    ctu_y = 128 * (ctu / a.ctu_cols);
+    fx0 = ctu_x + 64 * (quad & 1);
+    fy0 = ctu_y + 64 * (quad >> 1);
+  }
+};
 
 // Stage the reference lattice (ALT): rows 4i-1 (columns -4..63), columns 4i-1 (rows -1..63).
 __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
@@ -802,43 +840,53 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
   }
 }
 
+// Next-item prefetch (non-ALT): two quadrant windows in LDS.  The first wave of an item to
+// run out of tasks takes the next item from the device-wide counter and stages its window
+// into the other buffer while the remaining waves finish theirs, so neither the counter's
+// round trip nor the window's HBM latency stalls the whole workgroup between items (skipping
+// the staging altogether measured +1.2 %).  The ALT lattice leaves no LDS for a second buffer.
+template <bool ALT>
+constexpr bool kPrefetch = MIP_PREFETCH && !ALT;
+template <bool ALT>
+constexpr int kOrgTiles = kPrefetch<ALT> ? 2 : 1;
+constexpr int kCounterWords = 8;  // [parity]: next task, finished waves, item
+
 template <bool ALT>
 __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
+  constexpr bool PF = kPrefetch<ALT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint16_t *org = reinterpret_cast<uint16_t *>(smem);
-  uint16_t *ref = ALT ? org + kTileElems : org;
-  uint8_t *w = smem + (kTileElems + (ALT ? kLatElems : 0)) * 2;
+  uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles windows
+  uint16_t *lattice = org_buf + kOrgTiles<ALT> * kTileElems;
+  uint8_t *w = smem + (kOrgTiles<ALT> * kTileElems + (ALT ? kLatElems : 0)) * 2;
   uint8_t *zero = w + kTableBytes;
   uint8_t *waves = zero + kZeroBytes;
+  uint32_t *counters = reinterpret_cast<uint32_t *>(waves + kWaves * kWaveBytes);
 
   for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(w)[i] = a.tables[i];
   for (int i = threadIdx.x; i < kZeroBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
-  uint32_t *next_task = reinterpret_cast<uint32_t *>(waves + kWaves * kWaveBytes);
-  uint32_t *cur_item = next_task + 1;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int per_ctu = 4 * a.slices;
 
   // Persistent workgroups (as many as are resident) take items = (frame, CTU, quadrant,
   // slice) from a device-wide counter, in order: the hardware's static round-robin of
   // workgroups over XCDs and CUs cannot balance items of unequal cost (edge CTUs).
+  if (threadIdx.x < kCounterWords) counters[threadIdx.x] = threadIdx.x == 2 ? atomicAdd(a.queue, 1u) : 0u;
+  __syncthreads();
+  int par = 0;          // workgroup-uniform: parity of the item (window buffer, counter set)
+  bool staged = false;  // workgroup-uniform: the window of the current item is in LDS
   for (;;) {
-    if (threadIdx.x == 0) {
-      *cur_item = atomicAdd(a.queue, 1u);
-      *next_task = 0;
-    }
-    __syncthreads();
-    const uint32_t item = *cur_item;
+    uint32_t *next_task = counters + 4 * par, *finished = next_task + 1;
+    const uint32_t item = next_task[2];
     if (item >= a.nitems) break;  // workgroup-uniform
-    const int gx = item % per_ctu, ctu = a.ctu0 + (item / per_ctu) % a.nrange, frame = item / (per_ctu * a.nrange);
-    const int slice = gx % a.slices, quad = gx / a.slices;
-    const int ctu_x = 128 * (ctu % a.ctu_cols), ctu_y = 128 * (ctu / a.ctu_cols);
-    const int fx0 = ctu_x + 64 * (quad & 1), fy0 = ctu_y + 64 * (quad >> 1);
+    const ItemPos ip(a, item);
+    const int ctu = ip.ctu, frame = ip.frame, slice = ip.slice, quad = ip.quad, fx0 = ip.fx0, fy0 = ip.fy0;
     const size_t fofs = (size_t)frame * a.width * a.height;
-    const int var = (ctu_x + 128 > a.width ? 1 : 0) | (ctu_y + 128 > a.height ? 2 : 0);
+    const int var = (ip.ctu_x + 128 > a.width ? 1 : 0) | (ip.ctu_y + 128 > a.height ? 2 : 0);
     const int vq = var * 4 + quad, list = vq * a.slices + slice;
     const int tbase = a.list_begin[list], ntasks = a.list_begin[list + 1] - tbase;
+    uint16_t *org = org_buf + (PF ? par * kTileElems : 0);
+    uint16_t *ref = ALT ? lattice : org;
 
     // CUs not completely inside the frame (edge CTUs): MIP_COST_UNAVAILABLE, no search
     if (var) {
@@ -853,9 +901,11 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
       }
     }
     if (ntasks > 0) {  // workgroup-uniform
-      stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0);
-      if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0);
-      __syncthreads();
+      if (!PF || !staged) {
+        stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0);
+        if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0);
+        __syncthreads();
+      }
 
       const Ctx x{&a, org, ref, w, zero, waves + wave * kWaveBytes, ctu, frame, fx0, fy0};
       const RefTile<ALT> rt{ref};
@@ -889,7 +939,54 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
         if (clk && lane == 0 && t < kClockSlots) clk[t] = __builtin_readcyclecounter() - c0;
       }
     }
-    __syncthreads();  // the tile and cur_item are rewritten for the next item
+    // ---- next item: its index (and, PF, its window) go to the other parity's slots, which
+    // no wave reads during this item
+    if (PF) {
+      uint32_t *nxt = counters + 4 * (par ^ 1);
+      uint32_t r = 0;
+      if (lane == 0) r = atomicAdd(finished, 1u);
+      if (__builtin_amdgcn_readfirstlane(r) == 0) {  // wave-uniform: the first idle wave
+        uint32_t n = 0;
+        if (lane == 0) n = atomicAdd(a.queue, 1u);
+        const uint32_t nitem = __builtin_amdgcn_readfirstlane(n);
+        if (nitem < a.nitems) {
+          const ItemPos np(a, nitem);
+          const uint16_t *nframe = a.orig + (size_t)np.frame * a.width * a.height;
+          uint16_t *dst = org_buf + (par ^ 1) * kTileElems;
+          // loads in flight MIP_PF_BATCH at a time, then their stores
+          constexpr int NL = (kTileLoads + 63) / 64, NB = MIP_PF_BATCH;
+#pragma unroll 1
+          for (int k0 = 0; k0 < NL; k0 += NB) {
+            uint2 v[NB];
+#pragma unroll
+            for (int k = 0; k < NB; k++) {
+              const int i = lane + 64 * (k0 + k);
+              v[k] = i < kTileLoads ? tile_load(nframe, a.width, a.height, np.fx0, np.fy0, i) : make_uint2(0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < NB; k++) {
+              const int i = lane + 64 * (k0 + k);
+              if (i < kTileLoads) tile_store(dst, i, v[k]);
+            }
+          }
+        }
+        if (lane == 0) {
+          nxt[0] = 0;
+          nxt[1] = 0;
+          nxt[2] = nitem;
+        }
+      }
+      __syncthreads();  // the window and the counters of the next item are in place
+      staged = true;
+    } else {
+      __syncthreads();  // every wave is done with the window and the item's counters
+      if (threadIdx.x == 0) {
+        next_task[0] = 0;
+        next_task[2] = atomicAdd(a.queue, 1u);
+      }
+      __syncthreads();  // the next item is in place
+    }
+    if (PF) par ^= 1;  // (a loop-carried parity costs the ALT kernel ~30 VGPRs)
   }
   // The last workgroup to leave resets the counter pair for the next launch that uses it
   // (the host never runs two launches on one pair at the same time).
@@ -954,7 +1051,8 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
 int search_waves_per_group() { return kWaves; }
 
 size_t search_lds_bytes(bool alt) {
-  return (size_t)(kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes + (size_t)kWaves * kWaveBytes + 16;
+  return (size_t)((alt ? kOrgTiles<true> : kOrgTiles<false>) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
+         (size_t)kWaves * kWaveBytes + kCounterWords * 4;
 }
 
 int search_resident_groups(bool alt) {
