@@ -66,6 +66,9 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #ifndef MIP_PF_BATCH
 #define MIP_PF_BATCH 6  // window loads in flight per lane in the prefetching wave
 #endif
+#ifndef MIP_UV2_UNROLL
+#define MIP_UV2_UNROLL 2  // blocks per loop iteration, UV = 2 classes with H > 8 (A/B knob)
+#endif
 #ifndef MIP_WIN_UNROLL
 #define MIP_WIN_UNROLL 2  // windows of the vertical pass per loop iteration (A/B knob)
 #endif
@@ -504,7 +507,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
   } else if constexpr (G::UV == 2) {
     // Vertical pass (intra.cl:867-893) with two windows per 4x4 block: the row between
     // anchors k-1 and k is (prev + next + 1) >> 1.
-    constexpr int kUnroll = H <= 8 ? 2 : 1;
+    constexpr int kUnroll = H <= 8 ? 2 : MIP_UV2_UNROLL;
     constexpr int NBLK = (G::CHUNKED ? 4 : G::KV) / 2;  // blocks in [k0, k1)
     (void)k1;
 #pragma unroll kUnroll
