@@ -376,3 +376,48 @@ def test_async_host_calls_and_device_filter_scratch(gpu_available):
         assert np.array_equal(dc.cpu().numpy(), want[4:6])
     assert np.array_equal(o1["cost"], want[0:2])
     assert np.array_equal(o2["cost"], want[2:4])
+
+
+@pytest.mark.parametrize("w,h,filt,k", [(264, 200, None, 0), (136, 72, None, 0),
+                                        (392, 264, "filterFrame_2d_float_5x5_quarterCtu", 2)])
+def test_device_decisions_only_fused_argmin(gpu_available, w, h, filt, k):
+    """mip_search_device without a cost table (costs=False): the search keeps each CU's
+    argmin (cost << 5 | mode, atomicMin per task -- tasks that cut a CU's mode pairs meet in
+    one entry) and unpacks it; must equal the argmin of the oracle's table (ties to the lower
+    mode, unavailable CUs 0xff / MIP_COST_UNAVAILABLE), for 1..3-frame batches (different
+    task cuts per slice count)."""
+    import torch
+    n = 3
+    frames = synth_frames(w, h, n, 0xD0 + w, 1)
+    nct = layout.num_ctus(w, h)
+    want = []
+    for f in range(n):
+        refs = O.filter_frame(frames[f], filt, k) if filt else None
+        want.append(layout.best_modes(O.search(frames[f], refs), nct))
+    d = torch.from_numpy(frames.astype(np.int16)).cuda()
+    with MipEngine(w, h, max_batch=n, filter=filt, kernel_idx=k) as eng:
+        for nb in (1, 2, 3):
+            bm = torch.empty((nb, eng.cus_per_frame), dtype=torch.uint8, device="cuda")
+            bc = torch.empty((nb, eng.cus_per_frame), dtype=torch.int32, device="cuda")
+            assert eng.search_device(d[:nb], costs=False, best_mode=bm, best_cost=bc) is None
+            torch.cuda.synchronize()
+            for f in range(nb):
+                assert np.array_equal(bm[f].cpu().numpy(), want[f][0]), (nb, f)
+                assert np.array_equal(bc[f].cpu().numpy(), want[f][1]), (nb, f)
+        with pytest.raises(MipError):  # the packed argmin needs the cost output as scratch
+            eng.search_device(d[:1], costs=False, best_mode=bm[:1])
+
+
+def test_decisions_only_full_size_matches_table_argmin(gpu_available):
+    """1080p (the bench size), 2 frames: the fused decisions-only search gives exactly the
+    decision lists of the full cost table (best_mode_kernel over it)."""
+    W, H = 1920, 1080
+    frames = synth_frames(W, H, 2, 0xDEC, 0)
+    with MipEngine(W, H, max_batch=2) as eng:
+        full = eng.search(frames, best=True)
+        dec = eng.search(frames, costs=False, best=True)
+    assert "cost" not in dec
+    assert np.array_equal(dec["best_mode"], full["best_mode"])
+    assert np.array_equal(dec["best_cost"], full["best_cost"])
+    bm, bc = layout.best_modes(full["cost"][1], layout.num_ctus(W, H))
+    assert np.array_equal(dec["best_mode"][1], bm) and np.array_equal(dec["best_cost"][1], bc)

@@ -15,7 +15,7 @@ struct Job {      // one CU of a task (geometry resolved on the host: no divisio
   uint32_t cost;  // entry of mode 0 inside the CTU's cost block: shape offset + cu*2*modes
                   // (CU index in reference order, constants.h:1235-1354 / 1558-1631)
   uint8_t lx, ly; // CU origin inside the 64x64 quadrant
-  uint16_t pad;
+  uint16_t cu;    // CU index inside the CTU (reference order, 0..5379): decision entries
 };
 struct WaveTask {
   uint8_t cls;    // size class, kClassW/kClassH
@@ -47,7 +47,9 @@ constexpr int class_slots(int cls) { return 64 / ((kClassW[cls] / 4) * kClassV[c
 struct SearchArgs {
   const uint16_t *orig;   // [frames][height][width] original samples (distortion)
   const uint16_t *refs;   // reference-sample source: == orig, or the filtered frames
-  int32_t *cost;          // [frames][nctus][97840]  min(2*SAD, SATD)
+  int32_t *cost;          // [frames][nctus][97840]  min(2*SAD, SATD); null: decisions only
+  uint32_t *best;         // optional: [frames][nctus][5380] running argmin (cost << 5 | mode),
+                          // all ones at launch (atomicMin per task and CU)
   int32_t *sad;           // optional, same layout
   int32_t *satd;          // optional, same layout
   const WaveTask *tasks;  // per (quadrant, wave) task lists, concatenated
@@ -116,6 +118,9 @@ int search_waves_per_group();
 int search_resident_groups(bool alt_refs);
 hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, hipStream_t s);
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
+// packed argmin (SearchArgs::best) -> per-CU best mode / cost (k = 1 decision lists)
+hipError_t launch_unpack_best(const uint32_t *packed, uint8_t *best_mode, int32_t *best_cost, int total_cus,
+                              hipStream_t s);
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s);
 
 }  // namespace mipgpu

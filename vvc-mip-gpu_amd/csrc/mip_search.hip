@@ -690,7 +690,7 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
-template <int W, int H, int V, bool LAT>
+template <int W, int H, int V, bool LAT, bool DEC>
 __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, const WaveTask &task, int lane_in) {
   using G = Geo<W, H, V>;
   const int lane = opaque(lane_in);
@@ -734,6 +734,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   }
   wave_lds_sync();
 
+  uint32_t best = 0xffffffffu;  // DEC (decisions only): argmin over the task's pairs, cost << 5 | mode
 #pragma unroll 1
   for (int q = task.q0; q < task.q1; q++) {
     Acc acc;
@@ -770,11 +771,19 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       const size_t idx = cbase + 2 * q;
       // every CU of a task lies inside the frame (build_work); intra.cl:1166
       const int c0 = min(2 * (int)acc.sad0, (int)acc.satd0), c1 = min(2 * (int)acc.sad1, (int)acc.satd1);
-      *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
-      if (a.sad) *reinterpret_cast<int2 *>(a.sad + idx) = make_int2(acc.sad0, acc.sad1);
-      if (a.satd) *reinterpret_cast<int2 *>(a.satd + idx) = make_int2(acc.satd0, acc.satd1);
+      if constexpr (DEC) {
+        // costs < 2^23 (256 blocks x 32736): the packed order is cost, then the lower mode
+        best = min(best, min((uint32_t)c0 << 5 | (uint32_t)(2 * q), (uint32_t)c1 << 5 | (uint32_t)(2 * q + 1)));
+      } else {
+        *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
+        if (a.sad) *reinterpret_cast<int2 *>(a.sad + idx) = make_int2(acc.sad0, acc.sad1);
+        if (a.satd) *reinterpret_cast<int2 *>(a.satd + idx) = make_int2(acc.satd0, acc.satd1);
+      }
     }
   }
+  // tasks that cut a CU's mode pairs meet in one entry: atomicMin of the packed argmins
+  if (DEC && active && sub == G::S * G::V - 1)
+    atomicMin(a.best + ((size_t)x.frame * a.nctus + x.ctu) * MIP_CUS_PER_CTU + job.cu, best);
 }
 
 // Stage the quadrant window (rows -1..63, columns -4..63) of one frame into LDS, each
@@ -854,7 +863,8 @@ template <bool ALT>
 constexpr int kOrgTiles = kPrefetch<ALT> ? 2 : 1;
 constexpr int kCounterWords = 8;  // [parity]: next task, finished waves, item
 
-template <bool ALT>
+// DEC: decisions only -- no cost table, a per-CU packed argmin (SearchArgs::best).
+template <bool ALT, bool DEC>
 __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = kPrefetch<ALT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -892,7 +902,8 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     uint16_t *ref = ALT ? lattice : org;
 
     // CUs not completely inside the frame (edge CTUs): MIP_COST_UNAVAILABLE, no search
-    if (var) {
+    // (decisions only: their entries keep the launch's all-ones = unavailable)
+    if (var && !DEC) {
       const size_t cbase = ((size_t)frame * a.nctus + ctu) * (MIP_COSTS_PER_CTU / 4);
       const int f0 = a.fill_begin[vq], nf = a.fill_begin[vq + 1] - f0;
       const uint4 un = make_uint4(kUnavailable, kUnavailable, kUnavailable, kUnavailable);
@@ -927,7 +938,7 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   case idx:                                                                \
     static_assert(kClassW[idx] == W && kClassH[idx] == H, "class table");  \
     if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)                       \
-      run_task<W, H, kClassV[idx], ALT>(x, rt, task, lane);                \
+      run_task<W, H, kClassV[idx], ALT, DEC>(x, rt, task, lane);           \
     break;
           MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
           MIP_CASE(4, 32, 8) MIP_CASE(5, 8, 32) MIP_CASE(6, 16, 16) MIP_CASE(7, 16, 8)
@@ -1049,6 +1060,17 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
   }
 }
 
+// Packed argmin -> decision list of length 1 (the layout of best_mode_kernel with k = 1).
+__global__ __launch_bounds__(256) void unpack_best_kernel(const uint32_t *packed, uint8_t *best_mode, int32_t *best_cost,
+                                                          int total) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  const uint32_t p = packed[g];
+  const bool ok = p != 0xffffffffu;
+  if (best_mode) best_mode[g] = ok ? (uint8_t)(p & 31) : (uint8_t)0xff;
+  if (best_cost) best_cost[g] = ok ? (int32_t)(p >> 5) : kUnavailable;
+}
+
 }  // namespace
 
 int search_waves_per_group() { return kWaves; }
@@ -1058,15 +1080,21 @@ size_t search_lds_bytes(bool alt) {
          (size_t)kWaves * kWaveBytes + kCounterWords * 4;
 }
 
+template <bool ALT, bool DEC>
+static int resident_per_cu() {
+  int per_cu = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<ALT, DEC>, 64 * kWaves,
+                                                      search_lds_bytes(ALT)) == hipSuccess ? per_cu : 0;
+}
+
 int search_resident_groups(bool alt) {
-  int dev = 0, cus = 0, per_cu = 0;
+  int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  const hipError_t e = alt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<true>, 64 * kWaves,
-                                                                          search_lds_bytes(true))
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<false>, 64 * kWaves,
-                                                                          search_lds_bytes(false));
-  return e == hipSuccess && per_cu >= 1 ? cus * per_cu : 0;
+  // the full-table and the decisions-only kernel share the grid size
+  const int per_cu = alt ? std::min(resident_per_cu<true, false>(), resident_per_cu<true, true>())
+                         : std::min(resident_per_cu<false, false>(), resident_per_cu<false, true>());
+  return per_cu >= 1 ? cus * per_cu : 0;
 }
 
 hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, hipStream_t s) {
@@ -1077,10 +1105,23 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const size_t lds = search_lds_bytes(alt_refs);
-  if (alt_refs)
-    hipLaunchKernelGGL(mip_search_kernel<true>, dim3(groups), dim3(64 * kWaves), lds, s, a);
-  else
-    hipLaunchKernelGGL(mip_search_kernel<false>, dim3(groups), dim3(64 * kWaves), lds, s, a);
+  const bool dec = a.cost == nullptr;
+  if (dec && !a.best) return hipErrorInvalidValue;
+  if (alt_refs) {
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true>), dim3(groups), dim3(64 * kWaves), lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<true, false>), dim3(groups), dim3(64 * kWaves), lds, s, a);
+  } else {
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true>), dim3(groups), dim3(64 * kWaves), lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<false, false>), dim3(groups), dim3(64 * kWaves), lds, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_best(const uint32_t *packed, uint8_t *best_mode, int32_t *best_cost, int total_cus,
+                              hipStream_t s) {
+  if (!packed || total_cus < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(unpack_best_kernel, dim3((total_cus + 255) / 256), dim3(256), 0, s, packed, best_mode, best_cost,
+                     total_cus);
   return hipGetLastError();
 }
 

@@ -160,7 +160,8 @@ WorkLists build_work(int slices, int waves, int width, int height) {
     struct Piece { mipgpu::WaveTask t; double cost; };
     std::vector<Piece> pieces;
     std::vector<std::vector<mipgpu::Job>> cls_cus(mipgpu::kNumClasses);
-    for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+    int shape_cu0 = 0;  // first CU of the shape inside the CTU (reference order)
+    for (int s = 0; s < MIP_NUM_SHAPES; shape_cu0 += kShapes[s].ncu, s++) {
       if (!shape_selected(s)) continue;
       const mip_shape_desc &sd = kShapes[s];
       const int cls = mipgpu::size_class(sd.w, sd.h);
@@ -173,7 +174,7 @@ WorkLists build_work(int slices, int waves, int width, int height) {
           continue;
         }
         cls_cus[cls].push_back(mipgpu::Job{(uint32_t)(sd.cost_offset + cu * 2 * sd.modes), (uint8_t)(x % 64),
-                                           (uint8_t)(y % 64), 0});
+                                           (uint8_t)(y % 64), (uint16_t)(shape_cu0 + cu)});
       }
     }
     double total = 0;
@@ -523,7 +524,15 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
 static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
                               int32_t *d_best_cost, hipStream_t s, int ctu0 = 0, int nrange = -1) {
-  if (!e || !d_frames || !d_costs || nframes < 1) return fail("bad search arguments");
+  if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
+  // Decisions only (no cost table): the search keeps a per-CU argmin packed as
+  // (cost << 5 | mode) in d_best_cost and a small kernel unpacks it in place.
+  const bool decisions_only = d_costs == nullptr;
+  if (decisions_only) {
+    if (!d_best_cost) return fail("a search without d_costs needs d_best_cost (decisions only)");
+    if (e->opts.best_k != 1) return fail("a search without d_costs needs best_k == 1 (got %d)", e->opts.best_k);
+    if (d_sad || d_satd) return fail("a search without d_costs cannot produce SAD / SATD tables");
+  }
   if (nrange < 0) nrange = e->nctus - ctu0;
   if (ctu0 < 0 || nrange < 1 || ctu0 + nrange > e->nctus)
     return fail("CTU range [%d, %d) outside the frame's %d CTUs", ctu0, ctu0 + nrange, e->nctus);
@@ -545,6 +554,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.orig = d_frames;
   a.refs = alt ? refs : d_frames;
   a.cost = d_costs;
+  a.best = decisions_only ? reinterpret_cast<uint32_t *>(d_best_cost) : nullptr;
   a.sad = d_sad;
   a.satd = d_satd;
   const mip_engine::Work &work = pick_work(e, nframes, nrange);
@@ -586,6 +596,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
       }
     }
   }
+  if (decisions_only) HIP_TRY(hipMemsetAsync(d_best_cost, 0xff, (size_t)total_cus * 4, s));
   const int slot = (int)(e->queue_seq++ % mip_engine::kQueueSlots);
   if (e->queue_used[slot]) HIP_TRY(hipStreamWaitEvent(s, e->queue_done[slot], 0));
   a.queue = e->d_queue + 2 * slot;
@@ -605,7 +616,9 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
       fclose(f);
     }
   }
-  if (d_best || d_best_cost) {
+  if (decisions_only) {
+    HIP_TRY(mipgpu::launch_unpack_best(a.best, d_best, d_best_cost, (int)total_cus, s));
+  } else if (d_best || d_best_cost) {
     mipgpu::BestArgs b{d_costs, d_best, d_best_cost, (int)total_cus, e->opts.best_k};
     HIP_TRY(mipgpu::launch_best_modes(b, s));
   }
@@ -625,6 +638,7 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
                             int ctu_begin, int ctu_end, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
                             void *stream) {
   if (!e) return fail("engine is NULL");
+  if (!d_costs) return fail("d_costs is NULL");
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, nullptr, nullptr,
                             (hipStream_t)stream, ctu_begin, ctu_end - ctu_begin);
@@ -680,10 +694,13 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
         return -1;
       d_refs = e->d_refs + fo * fs;
     }
-    int32_t *d_costs = e->d_costs + fo * cpf;
+    // decisions only (no cost / SAD / SATD table requested, K = 1): the fused argmin, no table
+    const bool decisions_only = !costs_out && !sad_out && !satd_out && e->opts.best_k == 1 &&
+                                (best_mode_out || best_cost_out);
+    int32_t *d_costs = decisions_only ? nullptr : e->d_costs + fo * cpf;
     int32_t *d_sad = sad_out ? e->d_sad + fo * cpf : nullptr, *d_satd = satd_out ? e->d_satd + fo * cpf : nullptr;
     uint8_t *d_best = best_mode_out ? e->d_best + fo * upf : nullptr;
-    int32_t *d_best_cost = best_cost_out ? e->d_best_cost + fo * upf : nullptr;
+    int32_t *d_best_cost = best_cost_out || decisions_only ? e->d_best_cost + fo * upf : nullptr;
     if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp) != 0)
       return -1;
     HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));

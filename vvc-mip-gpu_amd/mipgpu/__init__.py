@@ -248,10 +248,13 @@ class MipEngine:
     def search_device(self, frames, refs=None, costs=None, sad=None, satd=None, best_mode=None,
                       best_cost=None, stream=None):
         """Asynchronous search on device tensors (torch, int16/uint16 [F,H,W]) on `stream`
-        (a torch.cuda.Stream; default: torch's current stream)."""
+        (a torch.cuda.Stream; default: torch's current stream).  costs=False: decisions only
+        (no cost table; needs best_cost, best_k = 1; returns None)."""
         import torch
         n = frames.shape[0]
-        if costs is None:
+        if costs is False:
+            costs = None
+        elif costs is None:
             costs = torch.empty((n, self.costs_per_frame), dtype=torch.int32, device=frames.device)
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
         _check(library().mip_search_device(self._h, _ptr(frames), _ptr(refs), n, _ptr(costs), _ptr(sad),
