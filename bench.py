@@ -306,6 +306,22 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize(dev)
             res["single_frame_ms"] = round(e0.elapsed_time(e1) / 20, 4)
+        if world == 1 and not args.no_latency:
+            # Decisions only (the serving path): the same B resident frames, no cost table --
+            # the per-CU argmin is fused into the search (mip_search_device with d_costs NULL).
+            bm = torch.empty((B, eng.cus_per_frame), dtype=torch.uint8, device=dev)
+            bc = torch.empty((B, eng.cus_per_frame), dtype=torch.int32, device=dev)
+            for _ in range(2):
+                eng.search_device(frames, costs=False, best_mode=bm, best_cost=bc, stream=stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(5):
+                eng.search_device(frames, costs=False, best_mode=bm, best_cost=bc, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            res["decisions_device"] = {"value": round(5 * B / (e0.elapsed_time(e1) * 1e-3), 1), "unit": "frames/s",
+                                       "note": "per-CU best mode + cost of the same resident frames, no cost table "
+                                               "(argmin fused into the search kernel), device time"}
         if world == 1:
             if not args.no_cpu_baseline:
                 res["cpu_baseline"] = cpu_baseline(W, H, args.seed)
@@ -324,7 +340,7 @@ def main():
             t0 = time.perf_counter()
             eng.search(host)
             pageable_fps = B / (time.perf_counter() - t0)
-            # decisions only: frames in, per-CU best mode + cost out (the cost tables stay in HBM)
+            # decisions only: frames in, per-CU best mode + cost out (no cost table: fused argmin)
             dout = {"best_mode": pinned_empty((B, eng.cus_per_frame), np.uint8),
                     "best_cost": pinned_empty((B, eng.cus_per_frame), np.int32)}
             eng.search(hp, costs=False, best=True, out=dout)

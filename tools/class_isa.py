@@ -15,7 +15,7 @@ subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-
                        "-I" + REPO + "/vvc-mip-gpu_amd/csrc", "-DMIP_ONLY_CLASS=%d" % cls, "--cuda-device-only", "-S",
                        "-o", out, REPO + "/vvc-mip-gpu_amd/csrc/mip_search.hip"], stderr=subprocess.DEVNULL)
 s = open(out).read()
-name = "_ZN6mipgpu12_GLOBAL__N_117mip_search_kernelILb%dELb0EEEvNS_10SearchArgsE:" % (1 if alt else 0)
+name = "_ZN6mipgpu12_GLOBAL__N_117mip_search_kernelILb%dELb0ELb%dEEEvNS_10SearchArgsE:" % ((1, 0) if alt else (0, 1))
 start = s.index(name)
 body = s[start:s.index("s_endpgm", start)].splitlines()
 labels = {m.group(1): i for i, l in enumerate(body) for m in [re.match(r"^(\.LBB\S+):", l)] if m}

@@ -60,8 +60,8 @@ constexpr ShapeStarts make_shape_starts() {
 static_assert(make_shape_starts().v[MIP_NUM_SHAPES] == MIP_CUS_PER_CTU, "shape table");
 __constant__ ShapeStarts c_shape_start = make_shape_starts();
 
-#ifndef MIP_PREFETCH
-#define MIP_PREFETCH 1  // next item's window loaded by the item's first idle wave (A/B knob)
+#ifndef MIP_PREFETCH_MIN_ITEMS
+#define MIP_PREFETCH_MIN_ITEMS 32  // items per workgroup from which a launch prefetches (A/B knob)
 #endif
 #ifndef MIP_PF_BATCH
 #define MIP_PF_BATCH 6  // window loads in flight per lane in the prefetching wave
@@ -852,25 +852,29 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
   }
 }
 
-// Next-item prefetch (non-ALT): two quadrant windows in LDS.  The first wave of an item to
-// run out of tasks takes the next item from the device-wide counter and stages its window
+// Next-item prefetch (PF, non-ALT): two quadrant windows in LDS.  The first wave of an item
+// to run out of tasks takes the next item from the device-wide counter and stages its window
 // into the other buffer while the remaining waves finish theirs, so neither the counter's
 // round trip nor the window's HBM latency stalls the whole workgroup between items (skipping
-// the staging altogether measured +1.2 %).  The ALT lattice leaves no LDS for a second buffer.
-template <bool ALT>
-constexpr bool kPrefetch = MIP_PREFETCH && !ALT;
-template <bool ALT>
-constexpr int kOrgTiles = kPrefetch<ALT> ? 2 : 1;
-constexpr int kCounterWords = 8;  // [parity]: next task, finished waves, item
+// the staging altogether measured +1.2 %).  Taking the next item early would unbalance the
+// end of a launch (a reserved item waits while other workgroups run dry: 16-frame launches
+// -1.4 % when every item was prefetched), so in the last two rounds of items the next one is
+// taken after the current one instead; launches with fewer than MIP_PREFETCH_MIN_ITEMS items
+// per workgroup do not prefetch at all (1-frame launches measured -9 % with the prefetching
+// kernel).  The ALT lattice leaves no LDS for a second window.
+template <bool ALT, bool PF>
+constexpr int kOrgTiles = PF && !ALT ? 2 : 1;
+constexpr int kCounterWords = 8;  // [parity]: next task, finished waves, item, item taken late
+constexpr uint32_t kTakeItem = 0xffffffffu;  // "take the next item after this one" (PF)
 
 // DEC: decisions only -- no cost table, a per-CU packed argmin (SearchArgs::best).
-template <bool ALT, bool DEC>
+template <bool ALT, bool DEC, bool PF_>
 __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
-  constexpr bool PF = kPrefetch<ALT>;
+  constexpr bool PF = PF_ && !ALT;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles windows
-  uint16_t *lattice = org_buf + kOrgTiles<ALT> * kTileElems;
-  uint8_t *w = smem + (kOrgTiles<ALT> * kTileElems + (ALT ? kLatElems : 0)) * 2;
+  uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles<ALT, PF> windows
+  uint16_t *lattice = org_buf + kOrgTiles<ALT, PF> * kTileElems;
+  uint8_t *w = smem + (kOrgTiles<ALT, PF> * kTileElems + (ALT ? kLatElems : 0)) * 2;
   uint8_t *zero = w + kTableBytes;
   uint8_t *waves = zero + kZeroBytes;
   uint32_t *counters = reinterpret_cast<uint32_t *>(waves + kWaves * kWaveBytes);
@@ -884,13 +888,21 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   // Persistent workgroups (as many as are resident) take items = (frame, CTU, quadrant,
   // slice) from a device-wide counter, in order: the hardware's static round-robin of
   // workgroups over XCDs and CUs cannot balance items of unequal cost (edge CTUs).
-  if (threadIdx.x < kCounterWords) counters[threadIdx.x] = threadIdx.x == 2 ? atomicAdd(a.queue, 1u) : 0u;
+  // (PF: the first item is taken like a late one, by the loop)
+  if (threadIdx.x < kCounterWords)
+    counters[threadIdx.x] = threadIdx.x != 2 ? 0u : (PF ? kTakeItem : atomicAdd(a.queue, 1u));
   __syncthreads();
   int par = 0;          // workgroup-uniform: parity of the item (window buffer, counter set)
-  bool staged = false;  // workgroup-uniform: the window of the current item is in LDS
   for (;;) {
     uint32_t *next_task = counters + 4 * par, *finished = next_task + 1;
-    const uint32_t item = next_task[2];
+    uint32_t item = next_task[2];
+    bool staged = PF;  // workgroup-uniform: the window of the item is in LDS
+    if (PF && item == kTakeItem) {  // near the end of the launch: take the item now
+      if (threadIdx.x == 0) next_task[3] = atomicAdd(a.queue, 1u);
+      __syncthreads();
+      item = next_task[3];
+      staged = false;
+    }
     if (item >= a.nitems) break;  // workgroup-uniform
     const ItemPos ip(a, item);
     const int ctu = ip.ctu, frame = ip.frame, slice = ip.slice, quad = ip.quad, fx0 = ip.fx0, fy0 = ip.fy0;
@@ -960,10 +972,14 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
       uint32_t r = 0;
       if (lane == 0) r = atomicAdd(finished, 1u);
       if (__builtin_amdgcn_readfirstlane(r) == 0) {  // wave-uniform: the first idle wave
-        uint32_t n = 0;
-        if (lane == 0) n = atomicAdd(a.queue, 1u);
+        // Taking the next item before this one is done is worth it only while many items
+        // are left: in the last rounds a reserved item would wait for this workgroup while
+        // others run dry, so there the next item is taken after the item (kTakeItem).
+        // (the queue head is about one round, gridDim.x items, past this item)
+        uint32_t n = kTakeItem;
+        if (lane == 0 && item + 3 * gridDim.x < a.nitems) n = atomicAdd(a.queue, 1u);
         const uint32_t nitem = __builtin_amdgcn_readfirstlane(n);
-        if (nitem < a.nitems) {
+        if (nitem < a.nitems) {  // (kTakeItem >= nitems)
           const ItemPos np(a, nitem);
           const uint16_t *nframe = a.orig + (size_t)np.frame * a.width * a.height;
           uint16_t *dst = org_buf + (par ^ 1) * kTileElems;
@@ -991,7 +1007,6 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
         }
       }
       __syncthreads();  // the window and the counters of the next item are in place
-      staged = true;
     } else {
       __syncthreads();  // every wave is done with the window and the item's counters
       if (threadIdx.x == 0) {
@@ -1075,25 +1090,26 @@ __global__ __launch_bounds__(256) void unpack_best_kernel(const uint32_t *packed
 
 int search_waves_per_group() { return kWaves; }
 
-size_t search_lds_bytes(bool alt) {
-  return (size_t)((alt ? kOrgTiles<true> : kOrgTiles<false>) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
+size_t search_lds_bytes(bool alt, bool pf) {
+  return (size_t)((pf && !alt ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
          (size_t)kWaves * kWaveBytes + kCounterWords * 4;
 }
 
-template <bool ALT, bool DEC>
+template <bool ALT, bool DEC, bool PF>
 static int resident_per_cu() {
   int per_cu = 0;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<ALT, DEC>, 64 * kWaves,
-                                                      search_lds_bytes(ALT)) == hipSuccess ? per_cu : 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<ALT, DEC, PF>, 64 * kWaves,
+                                                      search_lds_bytes(ALT, PF)) == hipSuccess ? per_cu : 0;
 }
 
 int search_resident_groups(bool alt) {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  // the full-table and the decisions-only kernel share the grid size
-  const int per_cu = alt ? std::min(resident_per_cu<true, false>(), resident_per_cu<true, true>())
-                         : std::min(resident_per_cu<false, false>(), resident_per_cu<false, true>());
+  // every variant of the kernel shares the grid size
+  const int per_cu = alt ? std::min(resident_per_cu<true, false, false>(), resident_per_cu<true, true, false>())
+                         : std::min({resident_per_cu<false, false, false>(), resident_per_cu<false, true, false>(),
+                                     resident_per_cu<false, false, true>(), resident_per_cu<false, true, true>()});
   return per_cu >= 1 ? cus * per_cu : 0;
 }
 
@@ -1101,18 +1117,25 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   if (args.slices < 1 || !args.queue || resident < 1) return hipErrorInvalidValue;
   SearchArgs a = args;
   if (a.ctu0 < 0 || a.nrange < 1 || a.ctu0 + a.nrange > a.nctus) return hipErrorInvalidValue;
-  a.nitems = (uint32_t)(4 * a.slices) * a.nrange * nframes;
+  const long long nitems = (long long)(4 * a.slices) * a.nrange * nframes;
+  if (nitems >= 0xffffffffLL) return hipErrorInvalidValue;
+  a.nitems = (uint32_t)nitems;
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
-  const size_t lds = search_lds_bytes(alt_refs);
   const bool dec = a.cost == nullptr;
   if (dec && !a.best) return hipErrorInvalidValue;
+  const bool pf = !alt_refs && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
+  const size_t lds = search_lds_bytes(alt_refs, pf);
+  const dim3 grid(groups), block(64 * kWaves);
   if (alt_refs) {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true>), dim3(groups), dim3(64 * kWaves), lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<true, false>), dim3(groups), dim3(64 * kWaves), lds, s, a);
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true, false>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<true, false, false>), grid, block, lds, s, a);
+  } else if (pf) {
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, true>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<false, false, true>), grid, block, lds, s, a);
   } else {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true>), dim3(groups), dim3(64 * kWaves), lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<false, false>), dim3(groups), dim3(64 * kWaves), lds, s, a);
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, false>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<false, false, false>), grid, block, lds, s, a);
   }
   return hipGetLastError();
 }
