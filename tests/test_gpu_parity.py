@@ -421,3 +421,27 @@ def test_decisions_only_full_size_matches_table_argmin(gpu_available):
     assert np.array_equal(dec["best_cost"], full["best_cost"])
     bm, bc = layout.best_modes(full["cost"][1], layout.num_ctus(W, H))
     assert np.array_equal(dec["best_mode"][1], bm) and np.array_equal(dec["best_cost"][1], bc)
+
+
+def test_prefetching_launch_equals_small_launches(gpu_available):
+    """Launches with >= 32 items per workgroup run the prefetching kernel variant (next item's
+    window staged by the first idle wave, late takes in the last rounds; mip_search.hip).
+    34 1080p frames in one launch (18 360 items) must give exactly the tables of the same
+    frames searched two at a time (the non-prefetching variant, pinned to the oracle by the
+    other tests), and the decisions-only variant of the big launch the argmin of its table."""
+    import torch
+    from mipgpu import topk_device
+    W, H, n = 1920, 1080, 34
+    frames = torch.from_numpy(synth_frames(W, H, n, 0x9F0, 0).astype(np.int16)).cuda()
+    with MipEngine(W, H, max_batch=n) as eng:
+        big = eng.search_device(frames)
+        small = torch.empty_like(big)
+        for f in range(0, n, 2):
+            eng.search_device(frames[f:f + 2], costs=small[f:f + 2])
+        bm = torch.empty((n, eng.cus_per_frame), dtype=torch.uint8, device="cuda")
+        bc = torch.empty((n, eng.cus_per_frame), dtype=torch.int32, device="cuda")
+        eng.search_device(frames, costs=False, best_mode=bm, best_cost=bc)
+        tm, tc = topk_device(big, W, H, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(big, small)
+        assert torch.equal(bm, tm[..., 0]) and torch.equal(bc, tc[..., 0])
