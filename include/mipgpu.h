@@ -121,7 +121,10 @@ int mip_wait(mip_engine *e, uint64_t ticket);
  * `stream` is a hipStream_t; NULL means the default (null) stream, as in HIP).
  * Asynchronous on `stream`.
  * d_refs NULL: originals, or the engine filter applied into engine scratch.
- * d_costs required; the optional outputs may be NULL. */
+ * d_costs NULL = decisions only (no cost table is written): needs d_best_cost and
+ * opts.best_k == 1, no SAD / SATD; the search kernel keeps every CU's argmin itself (packed
+ * in d_best_cost, unpacked in place).  mip_search_frames takes this path whenever no table
+ * (costs / SAD / SATD) is requested and best_k == 1.  The optional outputs may be NULL. */
 int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
                       int nframes, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
                       uint8_t *d_best_mode, int32_t *d_best_cost, void *stream);
