@@ -254,3 +254,30 @@ def test_truncated_input_fails(gpu_available, tmp_path):
              "--BatchFrames", "1"])
     assert r.returncode == 1
     assert "error while opening samples files" in r.stderr
+
+
+@pytest.mark.gpu
+@needs_cli
+def test_best_modes_of_unlogged_frames(gpu_available, tmp_path):
+    """--BestModes without --AllFrames / --BinaryLog: only frame 0's cost table is needed (the
+    reference's log), so frames 1.. are searched decisions-only (the argmin fused into the
+    search kernel, no cost table).  Every frame's decision rows must equal the oracle's argmin
+    (ties to the lower mode, unavailable CUs Mode -1)."""
+    import csv
+    W, H, N = 264, 200, 4
+    frames = synth_frames(W, H, N, 0xC16, 1)
+    write_csv(tmp_path / "in.csv", frames)
+    prefix = str(tmp_path / "out")
+    r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / "in.csv"), "-l", prefix, "--BatchFrames", "3",
+             "--BestModes", prefix + "_best.csv"])
+    assert r.returncode == 0, r.stdout + r.stderr
+    rows = list(csv.DictReader(open(prefix + "_best.csv")))
+    n = layout.num_ctus(W, H)
+    assert len(rows) == N * n * layout.CUS_PER_CTU
+    for f in range(N):
+        bm, bc = layout.best_modes(O.search(frames[f]), n)
+        got = rows[f * n * layout.CUS_PER_CTU:(f + 1) * n * layout.CUS_PER_CTU]
+        assert [int(x["Cost"]) for x in got] == bc.tolist(), f
+        shapes = [s for s in layout.SHAPES for _ in range(s.ncu)] * n
+        want = [(-1, -1) if m == 0xFF else (int(m) % s.modes, int(m >= s.modes)) for m, s in zip(bm, shapes)]
+        assert [(int(x["BestMode"]), int(x["Transposed"])) for x in got] == want, f
