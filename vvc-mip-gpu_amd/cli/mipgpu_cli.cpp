@@ -368,6 +368,56 @@ void write_cost_log(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, i
   for (const std::string &s : bufs) fwrite(s.data(), 1, s.size(), fp);
 }
 
+// Decision rows of one frame (--BestModes): K = 1 "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,
+// Transposed,Cost", K > 1 one row per rank "...,Rank,Mode,Transposed,Cost" (modes past the
+// CU's list omitted, unavailable CUs one row with -1); formatted by CTU chunks in parallel and
+// written in order, like the cost log.
+void write_best_rows(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, int ctu_cols, int frame, int K,
+                     const uint8_t *best, const int32_t *best_cost, int threads) {
+  const int chunk = 8;
+  const int nchunks = (nctus + chunk - 1) / chunk;
+  std::vector<std::string> bufs(nchunks);
+  auto work = [&](int c) {
+    std::string &s = bufs[c];
+    s.resize((size_t)chunk * MIP_CUS_PER_CTU_ABI * K * 72);
+    char *p = &s[0];
+    for (int ctu = c * chunk; ctu < std::min(nctus, (c + 1) * chunk); ctu++) {
+      size_t k = (size_t)ctu * MIP_CUS_PER_CTU_ABI;
+      for (const ShapeInfo &sh : shapes)
+        for (int cu = 0; cu < sh.ncu; cu++, k++) {
+          const size_t i0 = k * K;
+          const int x = 128 * (ctu % ctu_cols) + sh.x[cu], y = 128 * (ctu / ctu_cols) + sh.y[cu];
+          for (int r = 0; r < K; r++) {
+            const int m = best[i0 + r];
+            if (K > 1 && m == 0xff && best[i0] != 0xff) break;  // past the CU's modes
+            p = put_int(p, frame); *p++ = ',';
+            p = put_int(p, ctu); *p++ = ',';
+            memcpy(p, sh.name.data(), sh.name.size()); p += sh.name.size(); *p++ = ',';
+            p = put_int(p, sh.w); *p++ = ',';
+            p = put_int(p, sh.h); *p++ = ',';
+            p = put_int(p, cu); *p++ = ',';
+            p = put_int(p, x); *p++ = ',';
+            p = put_int(p, y); *p++ = ',';
+            if (K > 1) { p = put_int(p, r); *p++ = ','; }
+            p = put_int(p, m == 0xff ? -1 : m % sh.modes); *p++ = ',';
+            p = put_int(p, m == 0xff ? -1 : (m >= sh.modes)); *p++ = ',';
+            p = put_int(p, best_cost[i0 + r]); *p++ = '\n';
+            if (m == 0xff) break;  // unavailable CU: one row
+          }
+        }
+    }
+    s.resize(p - &s[0]);
+  };
+  const int nt = std::max(1, threads);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; t++)
+    pool.emplace_back([&, t] {
+      for (int c = t; c < nchunks; c += nt) work(c);
+    });
+  for (auto &th : pool) th.join();
+  for (const std::string &s : bufs) fwrite(s.data(), 1, s.size(), fp);
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -539,28 +589,9 @@ int main(int argc, char **argv) {
                   fseeko(bin_fp, base + (2LL * o.frames + f) * tab, SEEK_SET) == 0 &&
                   fwrite(sl.satd.data() + co, 4, cpf, bin_fp) == cpf;
         }
-        if (want_best) {
-          const int K = o.topk;
-          const uint8_t *best = sl.best.data() + i * upf;
-          const int32_t *best_cost = sl.best_cost.data() + i * upf;
-          for (int ctu = 0, k = 0; ctu < nctus; ctu++)
-            for (const ShapeInfo &sh : shapes)
-              for (int cu = 0; cu < sh.ncu; cu++, k++) {
-                const size_t i0 = ((size_t)ctu * MIP_CUS_PER_CTU_ABI + (k % MIP_CUS_PER_CTU_ABI)) * K;
-                const int x = 128 * (ctu % ctu_cols) + sh.x[cu], y = 128 * (ctu / ctu_cols) + sh.y[cu];
-                for (int r = 0; r < K; r++) {
-                  const int m = best[i0 + r];
-                  if (K > 1 && m == 0xff && best[i0] != 0xff) break;  // past the CU's modes
-                  if (K == 1)
-                    fprintf(best_fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x, y,
-                            m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
-                  else
-                    fprintf(best_fp, "%d,%d,%s,%d,%d,%d,%d,%d,%d,%d,%d,%d\n", f, ctu, sh.name.c_str(), sh.w, sh.h, cu, x,
-                            y, r, m == 0xff ? -1 : m % sh.modes, m == 0xff ? -1 : (m >= sh.modes), best_cost[i0 + r]);
-                  if (m == 0xff) break;  // unavailable CU: one row
-                }
-              }
-        }
+        if (want_best)
+          write_best_rows(best_fp, shapes, nctus, ctu_cols, f, o.topk, sl.best.data() + i * upf,
+                          sl.best_cost.data() + i * upf, threads);
       }
       if (!wok) return fail(write_failed);
       set_state(s, 0);
