@@ -325,18 +325,39 @@ struct ShapeInfo {
   std::vector<int> x, y;
 };
 
-// exportAllDistortionValues_File (main_aux_functions.h:735-798), formatted by CTU chunks
-// in parallel and written in order.
+// Rows formatted by CTU chunks on `threads` threads, written in chunk order; at most
+// `threads` chunk buffers exist at a time (an 8K frame's cost log is ~11 GB of text).
+// format(c, p) writes chunk c's rows at p and returns the end; chunk_bytes bounds them.
+template <class F>
+void write_chunks_in_order(FILE *fp, int nchunks, size_t chunk_bytes, int threads, F &&format) {
+  const int nt = std::max(1, threads);
+  std::vector<std::vector<char>> bufs(std::min(nt, nchunks));
+  std::vector<size_t> used(bufs.size());
+  for (int c0 = 0; c0 < nchunks; c0 += nt) {
+    const int n = std::min(nt, nchunks - c0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < n; t++)
+      pool.emplace_back([&, t] {
+        bufs[t].resize(chunk_bytes);
+        used[t] = format(c0 + t, bufs[t].data()) - bufs[t].data();
+      });
+    for (auto &th : pool) th.join();
+    for (int t = 0; t < n; t++) fwrite(bufs[t].data(), 1, used[t], fp);
+  }
+}
+
+// Bound on a row of either format: every int field at its widest (11 characters; W, H, CU,
+// Mode, Rank, Transposed are shorter), a shape name of <= 16 characters, separators and the
+// newline: <= 102 bytes for a cost-log row, <= 95 for a decision row.
+constexpr size_t kMaxRowBytes = 128;
+
+// exportAllDistortionValues_File (main_aux_functions.h:735-798).
 void write_cost_log(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, int W, const int32_t *cost,
                     const int32_t *sad, const int32_t *satd, int threads) {
   const int ctu_cols = (W + 127) / 128;
   const int chunk = 8;
   const int nchunks = (nctus + chunk - 1) / chunk;
-  std::vector<std::string> bufs(nchunks);
-  auto work = [&](int c) {
-    std::string &s = bufs[c];
-    s.resize((size_t)chunk * MIP_COSTS_PER_CTU_ABI * 80);
-    char *p = &s[0];
+  write_chunks_in_order(fp, nchunks, (size_t)chunk * MIP_COSTS_PER_CTU_ABI * kMaxRowBytes, threads, [&](int c, char *p) {
     for (int ctu = c * chunk; ctu < std::min(nctus, (c + 1) * chunk); ctu++) {
       const int cx = 128 * (ctu % ctu_cols), cy = 128 * (ctu / ctu_cols);
       for (const ShapeInfo &sh : shapes)
@@ -356,31 +377,18 @@ void write_cost_log(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, i
             p = put_int(p, cost[idx]); *p++ = '\n';
           }
     }
-    s.resize(p - &s[0]);
-  };
-  const int nt = std::max(1, threads);
-  std::vector<std::thread> pool;
-  for (int t = 0; t < nt; t++)
-    pool.emplace_back([&, t] {
-      for (int c = t; c < nchunks; c += nt) work(c);
-    });
-  for (auto &th : pool) th.join();
-  for (const std::string &s : bufs) fwrite(s.data(), 1, s.size(), fp);
+    return p;
+  });
 }
 
 // Decision rows of one frame (--BestModes): K = 1 "Frame,CTU,cuSizeName,W,H,CU,X,Y,BestMode,
 // Transposed,Cost", K > 1 one row per rank "...,Rank,Mode,Transposed,Cost" (modes past the
-// CU's list omitted, unavailable CUs one row with -1); formatted by CTU chunks in parallel and
-// written in order, like the cost log.
+// CU's list omitted, unavailable CUs one row with -1), formatted like the cost log.
 void write_best_rows(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, int ctu_cols, int frame, int K,
                      const uint8_t *best, const int32_t *best_cost, int threads) {
   const int chunk = 8;
   const int nchunks = (nctus + chunk - 1) / chunk;
-  std::vector<std::string> bufs(nchunks);
-  auto work = [&](int c) {
-    std::string &s = bufs[c];
-    s.resize((size_t)chunk * MIP_CUS_PER_CTU_ABI * K * 72);
-    char *p = &s[0];
+  write_chunks_in_order(fp, nchunks, (size_t)chunk * MIP_CUS_PER_CTU_ABI * K * kMaxRowBytes, threads, [&](int c, char *p) {
     for (int ctu = c * chunk; ctu < std::min(nctus, (c + 1) * chunk); ctu++) {
       size_t k = (size_t)ctu * MIP_CUS_PER_CTU_ABI;
       for (const ShapeInfo &sh : shapes)
@@ -406,16 +414,8 @@ void write_best_rows(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, 
           }
         }
     }
-    s.resize(p - &s[0]);
-  };
-  const int nt = std::max(1, threads);
-  std::vector<std::thread> pool;
-  for (int t = 0; t < nt; t++)
-    pool.emplace_back([&, t] {
-      for (int c = t; c < nchunks; c += nt) work(c);
-    });
-  for (auto &th : pool) th.join();
-  for (const std::string &s : bufs) fwrite(s.data(), 1, s.size(), fp);
+    return p;
+  });
 }
 
 }  // namespace
