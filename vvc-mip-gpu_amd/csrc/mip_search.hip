@@ -66,6 +66,9 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #ifndef MIP_PF_BATCH
 #define MIP_PF_BATCH 6  // window loads in flight per lane in the prefetching wave
 #endif
+#ifndef MIP_PHASEA_BATCH_NCS
+#define MIP_PHASEA_BATCH_NCS 2  // column sets from which phase A reads its B operands up front (A/B knob)
+#endif
 #ifndef MIP_UV2_UNROLL
 #define MIP_UV2_UNROLL 2  // blocks per loop iteration, UV = 2 classes with H > 8 (A/B knob)
 #endif
@@ -645,10 +648,18 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
       pofs = 0;
     }
     const h4 av = *reinterpret_cast<const h4 *>(abase + jofs * 16);
+    // classes with many column sets (one row block): all B operands read up front, so the
+    // MFMAs do not each wait for an LDS read (partial tasks read unused CU-table entries)
+    constexpr bool BATCH_B = NRB == 1 && NCS >= MIP_PHASEA_BATCH_NCS;
+    h4 bvs[BATCH_B ? NCS : 1];
+    if constexpr (BATCH_B) {
+#pragma unroll
+      for (int cs = 0; cs < NCS; cs++) bvs[cs] = *reinterpret_cast<const h4 *>(bbase + cs * 8 * kEntryBytes);
+    }
 #pragma unroll
     for (int cs = 0; cs < NCS; cs++) {
       if (cs > 0 && 8 * cs >= ncu) break;  // wave-uniform: partial last task
-      const h4 bv = *reinterpret_cast<const h4 *>(bbase + cs * 8 * kEntryBytes);
+      const h4 bv = BATCH_B ? bvs[BATCH_B ? cs : 0] : *reinterpret_cast<const h4 *>(bbase + cs * 8 * kEntryBytes);
       const f4 d = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bv, cin, 0, 0, 0);
       // columns of slots >= ncu hold garbage; they land in unused scratch columns unless
       // the class has fewer than 8 slots
