@@ -370,6 +370,18 @@ struct Acc {
   }
 };
 
+// Both modes' sums in the two 16-bit halves of one register, for CUs of at most two 4x4
+// blocks (4x4, 8x4, 4x8): per mode SAD <= 2 * 16368 and SATD <= 2 * 32736 < 2^16, so plain
+// 32-bit adds (and the DPP group sums) never carry across the halves, and
+// min(2 * SAD, SATD) is one packed shift and one packed min.
+struct PackedAcc {
+  uint32_t sad = 0, satd = 0;
+  __device__ __forceinline__ void add(u2 s, u2 t) {
+    sad += as_u32(s);
+    satd += as_u32(t);
+  }
+};
+
 // Reduced prediction of the lane's CU in the wave scratch: both modes of the pair per dword,
 // stored position (k, kx) at k*R + kx (rows offset by `k0` for the second half of a chunked
 // class).
@@ -474,9 +486,9 @@ struct OrigRows {
 // Walk one strip of one CU for one mode pair over upsampling windows [k0, k1) (rows for
 // UV == 1 and 4x4): prediction rows (upsampling, intra.cl:815-912) streamed through the
 // block transform.  `prev` is the anchor row above window k0 (vertical pass state).
-template <int W, int H, int V, bool LAT, class RED>
+template <int W, int H, int V, bool LAT, class RED, class ACC>
 __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &rt, const OrigRows<H> &orig,
-                                           const RED &red, int x0, int k0, int k1, s2 (&prev)[4], Acc &acc) {
+                                           const RED &red, int x0, int k0, int k1, s2 (&prev)[4], ACC &acc) {
   using G = Geo<W, H, V>;
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
@@ -748,7 +760,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   uint32_t best = 0xffffffffu;  // DEC (decisions only): argmin over the task's pairs, cost << 5 | mode
 #pragma unroll 1
   for (int q = task.q0; q < task.q1; q++) {
-    Acc acc;
+    std::conditional_t<(W * H <= 32), PackedAcc, Acc> acc;
     s2 prev[4];
 #pragma unroll
     for (int cc = 0; cc < 4; cc++) prev[cc] = top[cc];
@@ -774,21 +786,31 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
     wave_lds_sync();  // the scratch is rewritten by the next pair
     // ---- combine strips and row parts of one CU (adjacent lanes) into its last lane
     constexpr int GS = G::S * G::V;
-    acc.sad0 = group_sum<GS>(acc.sad0);
-    acc.sad1 = group_sum<GS>(acc.sad1);
-    acc.satd0 = group_sum<GS>(acc.satd0);
-    acc.satd1 = group_sum<GS>(acc.satd1);
+    uint32_t sad0, sad1, satd0, satd1;
+    int c0, c1;  // min(2 * SAD, SATD) of the pair's modes (intra.cl:1166)
+    if constexpr (W * H <= 32) {
+      const uint32_t sp = group_sum<GS>(acc.sad), tp = group_sum<GS>(acc.satd);
+      const uint32_t cp = as_u32(__builtin_elementwise_min(as_u2(sp) << (u2){1, 1}, as_u2(tp)));
+      c0 = (int)(cp & 0xffff);
+      c1 = (int)(cp >> 16);
+      sad0 = sp & 0xffff, sad1 = sp >> 16, satd0 = tp & 0xffff, satd1 = tp >> 16;
+    } else {
+      sad0 = group_sum<GS>(acc.sad0);
+      sad1 = group_sum<GS>(acc.sad1);
+      satd0 = group_sum<GS>(acc.satd0);
+      satd1 = group_sum<GS>(acc.satd1);
+      c0 = min(2 * (int)sad0, (int)satd0);
+      c1 = min(2 * (int)sad1, (int)satd1);
+    }
     if (active && sub == GS - 1) {
-      const size_t idx = cbase + 2 * q;
-      // every CU of a task lies inside the frame (build_work); intra.cl:1166
-      const int c0 = min(2 * (int)acc.sad0, (int)acc.satd0), c1 = min(2 * (int)acc.sad1, (int)acc.satd1);
+      const size_t idx = cbase + 2 * q;  // every CU of a task lies inside the frame (build_work)
       if constexpr (DEC) {
         // costs < 2^23 (256 blocks x 32736): the packed order is cost, then the lower mode
         best = min(best, min((uint32_t)c0 << 5 | (uint32_t)(2 * q), (uint32_t)c1 << 5 | (uint32_t)(2 * q + 1)));
       } else {
         *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
-        if (a.sad) *reinterpret_cast<int2 *>(a.sad + idx) = make_int2(acc.sad0, acc.sad1);
-        if (a.satd) *reinterpret_cast<int2 *>(a.satd + idx) = make_int2(acc.satd0, acc.satd1);
+        if (a.sad) *reinterpret_cast<int2 *>(a.sad + idx) = make_int2(sad0, sad1);
+        if (a.satd) *reinterpret_cast<int2 *>(a.satd + idx) = make_int2(satd0, satd1);
       }
     }
   }
