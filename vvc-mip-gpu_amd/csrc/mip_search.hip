@@ -69,6 +69,9 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #ifndef MIP_PHASEA_BATCH_NCS
 #define MIP_PHASEA_BATCH_NCS 2  // column sets from which phase A reads its B operands up front (A/B knob)
 #endif
+#ifndef MIP_ACC_PAIR
+#define MIP_ACC_PAIR 1  // blocks accumulated in pairs before unpacking (A/B knob)
+#endif
 #ifndef MIP_UV2_UNROLL
 #define MIP_UV2_UNROLL 2  // blocks per loop iteration, UV = 2 classes with H > 8 (A/B knob)
 #endif
@@ -362,12 +365,35 @@ __device__ __forceinline__ void block_finish(const BlockAcc &b, u2 &sad, u2 &sat
 // Packed block results -> 32-bit per-mode accumulators.
 struct Acc {
   uint32_t sad0 = 0, sad1 = 0, satd0 = 0, satd1 = 0;
+#if MIP_ACC_PAIR
+  // blocks are added in pairs: two blocks' packed sums still fit 16 bits per mode
+  // (SAD <= 32736, SATD <= 65472), so a pair costs two adds + the four unpacking dot2
+  u2 ps{0, 0}, pt{0, 0};
+  bool have = false;
+  __device__ __forceinline__ void unpack(u2 sad, u2 satd) {
+    sad0 = __builtin_amdgcn_udot2(sad, (u2){1, 0}, sad0, false);
+    sad1 = __builtin_amdgcn_udot2(sad, (u2){0, 1}, sad1, false);
+    satd0 = __builtin_amdgcn_udot2(satd, (u2){1, 0}, satd0, false);
+    satd1 = __builtin_amdgcn_udot2(satd, (u2){0, 1}, satd1, false);
+  }
+  __device__ __forceinline__ void add(u2 sad, u2 satd) {
+    if (have) unpack(as_u2(as_u32(ps) + as_u32(sad)), as_u2(as_u32(pt) + as_u32(satd)));
+    else ps = sad, pt = satd;
+    have = !have;
+  }
+  __device__ __forceinline__ void flush() {
+    if (have) unpack(ps, pt);
+    have = false;
+  }
+#else
   __device__ __forceinline__ void add(u2 sad, u2 satd) {
     sad0 = __builtin_amdgcn_udot2(sad, (u2){1, 0}, sad0, false);
     sad1 = __builtin_amdgcn_udot2(sad, (u2){0, 1}, sad1, false);
     satd0 = __builtin_amdgcn_udot2(satd, (u2){1, 0}, satd0, false);
     satd1 = __builtin_amdgcn_udot2(satd, (u2){0, 1}, satd1, false);
   }
+  __device__ __forceinline__ void flush() {}
+#endif
 };
 
 // Both modes' sums in the two 16-bit halves of one register, for CUs of at most two 4x4
@@ -795,6 +821,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       c1 = (int)(cp >> 16);
       sad0 = sp & 0xffff, sad1 = sp >> 16, satd0 = tp & 0xffff, satd1 = tp >> 16;
     } else {
+      acc.flush();
       sad0 = group_sum<GS>(acc.sad0);
       sad1 = group_sum<GS>(acc.sad1);
       satd0 = group_sum<GS>(acc.satd0);
