@@ -21,7 +21,7 @@ from mipgpu import MipEngine  # noqa: E402
 from mipgpu.synth import synth_frames  # noqa: E402
 
 CLASSES = ["64x64", "32x32", "32x16", "16x32", "32x8", "8x32", "16x16", "16x8", "8x16", "32x4", "4x32",
-           "16x4", "4x16", "8x8", "8x4", "4x8", "4x4", "32x8v2", "16x16v4", "16x8v2"]
+           "16x4", "4x16", "8x8", "8x4", "4x8", "4x4", "32x8v2", "16x16v4", "16x8v2", "8x16v4"]
 W, H, B, SLOTS = 1920, 1080, 8, 128
 frames = torch.from_numpy(synth_frames(W, H, B, 0x1080, 0).astype(np.int16)).cuda()
 eng = MipEngine(W, H, max_batch=B)

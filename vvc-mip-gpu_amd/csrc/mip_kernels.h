@@ -26,16 +26,17 @@ struct WaveTask {
 
 // Size classes: W x H with V row parts per CU.  Classes 0-16 are the base class of each CU
 // size (row parts: classes with few CUs per quadrant split each CU's rows over V lanes per
-// strip so that a task still fills the wave); 17-19 are variants with more row parts, used
+// strip so that a task still fills the wave); 17-20 are variants with more row parts, used
 // for the remainder group of a class whose CU count per quadrant is not a multiple of its
-// task size (e.g. 28 CUs of 32x8 = 3 tasks of 8 + one task of 4 CUs with V = 2).
-constexpr int kNumClasses = 20;
+// task size (e.g. 28 CUs of 32x8 = 3 tasks of 8 + one task of 4 CUs with V = 2; 84 CUs of
+// 8x16 = 2 tasks of 32 + three tasks of 7, 7, 6 CUs with V = 4).
+constexpr int kNumClasses = 21;
 constexpr int kNumBaseClasses = 17;
-constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 16, 4, 8, 8, 4, 4, 32, 16, 16};
-constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4, 8, 16, 8};
-constexpr int kClassV[kNumClasses] = {4, 2, 2, 4, 1, 1, 2, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2};
-constexpr int kClassVariant[kNumClasses] = {-1, -1, -1, -1, 17, -1, 18, 19, -1, -1, -1, -1, -1, -1, -1, -1, -1,
-                                            -1, -1, -1};  // remainder-task class of a base class
+constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 16, 4, 8, 8, 4, 4, 32, 16, 16, 8};
+constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4, 8, 16, 8, 16};
+constexpr int kClassV[kNumClasses] = {4, 2, 2, 4, 1, 1, 2, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2, 4};
+constexpr int kClassVariant[kNumClasses] = {-1, -1, -1, -1, 17, -1, 18, 19, 20, -1, -1, -1, -1, -1, -1, -1, -1,
+                                            -1, -1, -1, -1};  // remainder-task class of a base class
 constexpr int size_class(int w, int h) {  // base class of a CU size
   for (int i = 0; i < kNumBaseClasses; i++)
     if (kClassW[i] == w && kClassH[i] == h) return i;

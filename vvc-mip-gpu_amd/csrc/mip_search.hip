@@ -182,7 +182,8 @@ struct Geo {
   static constexpr int V = VP;                        // row parts per CU
   static constexpr int SLOTS = 64 / (S * V);          // CUs per task
   static constexpr int KV = R / V;                    // upsampling windows per row part
-  static constexpr bool CHUNKED = SID == 2 && UH == 1;  // 8xH: reduced rows in two halves
+  // 8xH: the reduced predictions of all the task's CUs do not fit the scratch: two halves
+  static constexpr bool CHUNKED = SID == 2 && UH == 1 && 64 / (S * V) * (64 + 4) > kScratchWords;
   static constexpr int CPOS = CHUNKED ? 32 : NOUT;    // scratch positions per chunk
   // Scratch rows: classes with horizontal interpolation (UH > 1) keep the anchor row's left
   // boundary sample in front of each reduced row (position k*RP, reduced (k, kx) at
@@ -1018,7 +1019,7 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
           MIP_CASE(12, 4, 16) MIP_CASE(13, 8, 8) MIP_CASE(14, 8, 4) MIP_CASE(15, 4, 8)
           MIP_CASE(16, 4, 4)
           // row-part variants for remainder tasks (mip_kernels.h)
-          MIP_CASE(17, 32, 8) MIP_CASE(18, 16, 16) MIP_CASE(19, 16, 8)
+          MIP_CASE(17, 32, 8) MIP_CASE(18, 16, 16) MIP_CASE(19, 16, 8) MIP_CASE(20, 8, 16)
 #undef MIP_CASE
           default: break;
         }

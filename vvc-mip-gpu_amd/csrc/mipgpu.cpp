@@ -186,11 +186,18 @@ WorkLists build_work(int slices, int waves, int width, int height) {
       const int modes = sid == 2 ? 6 : (sid == 1 ? 8 : 16);
       // groups (class, CUs): full tasks plus a remainder task of the class's row-part variant
       // when the remainder fits it; otherwise equal-sized groups
+      // (variant tasks replace one base task when they occupy fewer lane-blocks: a task of
+      // V row parts gives every lane H / (4 V) blocks per mode pair)
       std::vector<std::pair<int, int>> groups;
       const int var = mipgpu::kClassVariant[cls], rem = nv % slots;
-      if (rem > 0 && var >= 0 && rem <= mipgpu::class_slots(var)) {
+      const int nvar = var >= 0 ? (rem + mipgpu::class_slots(var) - 1) / mipgpu::class_slots(var) : 0;
+      if (rem > 0 && var >= 0 && nvar * mipgpu::kClassV[cls] < mipgpu::kClassV[var]) {
         for (int g = 0; g < nv / slots; g++) groups.push_back({cls, slots});
-        groups.push_back({var, rem});
+        for (int g = 0, at = 0; g < nvar; g++) {
+          const int n = (rem - at) / (nvar - g);
+          groups.push_back({var, n});
+          at += n;
+        }
       } else {
         const int ng = (nv + slots - 1) / slots;
         for (int g = 0, at = 0; g < ng; g++) {
