@@ -99,3 +99,15 @@ def test_filter_kernels_are_outer_product_plus_centre(name, ks, n):
         want = np.outer(t, t)
         want[ks // 2, ks // 2] += d
         assert np.array_equal(k, want) and (k == k.T).all()
+
+
+def test_torch_synth_matches_numpy_generator():
+    """bench.py generates its frames with torch on the GPU (synth_frames_torch); they must be
+    the frames of the numpy / C generator (large seeds: the uint64 wrap-around)."""
+    import torch  # noqa: F401
+    from mipgpu.synth import synth_frames, synth_frames_torch
+    for kind, seed in ((0, 0x1080), (0, 0x1080 + 7 * 1000003), (1, 0xFFFFFFFFFFF0), (2, 5)):
+        a = synth_frames(136, 72, 2, seed, kind)
+        b = synth_frames_torch(136, 72, 2, seed, kind).numpy().astype(np.uint16)
+        assert np.array_equal(a, b), (kind, seed)
+
