@@ -34,6 +34,13 @@ typedef short s2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u2 __attribute__((ext_vector_type(2)));
 
 constexpr int kThreads = 128;  // per tile: thread t owns columns 4(t&31).. +3, rows 8(t>>5).. +7
+#ifndef MIP_FILTER_TPW
+#define MIP_FILTER_TPW 1
+#endif
+constexpr int kTPW = MIP_FILTER_TPW;  // tiles per workgroup (128 threads each); 2 and 4 measured slower
+#ifndef MIP_FILTER_NT
+#define MIP_FILTER_NT 1  // filtered samples stored non-temporally (streamed out, -3 % time)
+#endif
 constexpr int kCO = 8;         // LDS column of tile column 0 (interior rows 16-byte aligned)
 constexpr int kTWP = 144;      // LDS row pitch in samples
 
@@ -113,54 +120,43 @@ __device__ __forceinline__ short inner_value(const uint16_t *in, int x, int y, i
 }
 
 // Stage the tile (+halo) in LDS: interior rows with 16-byte loads when the rows are
-// 16-byte aligned (W % 8 == 0), halo cells one by one with the reference's gates.
+// 16-byte aligned (W % 8 == 0), halo cells one by one with the reference's gates.  Every
+// phase issues all of a thread's loads before its first LDS store, so a workgroup waits for
+// HBM once per phase, not once per load (a load -> store loop waits for every load).
 // Returns whether this thread stored an invalid (-1) cell.
 template <int RAD, bool SEP>
 __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, int qy, int W, int H) {
   constexpr int TW = 128 + 2 * RAD;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x % kThreads;
   bool invalid = false;
   // Interior tile: with a margin of one tile / 16 samples to every frame border, every
   // gate of every filter (tap_valid / sep_fetch / inner_value) admits every cell, so the
   // tile and its halo are plain samples: rows -RAD..31+RAD, columns -8..135 as 16-byte
   // loads (the LDS row pitch is exactly those 144 columns).
   if ((W & 7) == 0 && qx >= 128 && qy >= 32 && qx + 144 <= W - 2 && qy + 40 <= H - 2) {
-    constexpr int NV = (32 + 2 * RAD) * (kTWP / 8);
-    for (int i = t; i < NV; i += kThreads) {
-      const int r = i / (kTWP / 8), k = i - r * (kTWP / 8);
-      *reinterpret_cast<uint4 *>(tile + r * kTWP + 8 * k) =
-          *reinterpret_cast<const uint4 *>(in + (size_t)(qy - RAD + r) * W + qx - 8 + 8 * k);
+    constexpr int NV = (32 + 2 * RAD) * (kTWP / 8), NPT = (NV + kThreads - 1) / kThreads;
+    uint4 v[NPT];
+#pragma unroll
+    for (int p = 0; p < NPT; p++) {
+      // the last round's spare threads repeat chunk NV - 1 (same value, same LDS slot)
+      const int i = min(t + p * kThreads, NV - 1), r = i / (kTWP / 8), k = i - r * (kTWP / 8);
+      v[p] = *reinterpret_cast<const uint4 *>(in + (size_t)(qy - RAD + r) * W + qx - 8 + 8 * k);
+    }
+#pragma unroll
+    for (int p = 0; p < NPT; p++) {
+      const int i = min(t + p * kThreads, NV - 1), r = i / (kTWP / 8), k = i - r * (kTWP / 8);
+      *reinterpret_cast<uint4 *>(tile + r * kTWP + 8 * k) = v[p];
     }
     return false;
   }
-  if ((W & 7) == 0) {
+  // Halo: RAD rows above and below (corners included), RAD columns left and right --
+  // gathered first, so its loads are in flight with the tile's; stored last.
+  constexpr int NROW = 2 * RAD * TW, NHALO = NROW + 2 * RAD * 32, NPH = (NHALO + kThreads - 1) / kThreads;
+  short hv[NPH];
+  int hidx[NPH];
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-      const int i = p * kThreads + t, r = i >> 4, k = i & 15;
-      const int y = qy + r, x = qx + 8 * k;
-      short *dst = tile + (r + RAD) * kTWP + kCO + 8 * k;
-      if (y < H && x + 8 <= W) {
-        *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<const uint4 *>(in + (size_t)y * W + x);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; e++) {
-          const short v = inner_value<RAD, SEP>(in, x + e, y, W, H);
-          invalid |= v < 0;
-          dst[e] = v;
-        }
-      }
-    }
-  } else {
-    for (int i = t; i < 32 * 128; i += kThreads) {
-      const int r = i >> 7, c = i & 127;
-      const short v = inner_value<RAD, SEP>(in, qx + c, qy + r, W, H);
-      invalid |= v < 0;
-      tile[(r + RAD) * kTWP + kCO + c] = v;
-    }
-  }
-  // Halo: RAD rows above and below (corners included), RAD columns left and right.
-  constexpr int NROW = 2 * RAD * TW, NHALO = NROW + 2 * RAD * 32;
-  for (int i = t; i < NHALO; i += kThreads) {
+  for (int p = 0; p < NPH; p++) {
+    const int i = min(t + p * kThreads, NHALO - 1);  // spare threads repeat the last cell
     int ty, tc;
     if (i < NROW) {
       const int r = i / TW;
@@ -172,9 +168,51 @@ __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, i
       tc = q < RAD ? q - RAD : 128 + q - RAD;
     }
     const bool fetch = SEP ? sep_fetch<RAD>(qx, qy, ty, tc, W, H) : tap_valid(RAD, qx, qy, ty, tc, W, H);
-    const short v = fetch ? (short)in[(long long)(qy + ty) * W + qx + tc] : (SEP && RAD == 1 ? 0 : -1);
-    invalid |= v < 0;
-    tile[(ty + RAD) * kTWP + kCO + tc] = v;
+    hv[p] = fetch ? (short)in[(long long)(qy + ty) * W + qx + tc] : (SEP && RAD == 1 ? 0 : -1);
+    hidx[p] = (ty + RAD) * kTWP + kCO + tc;
+  }
+  if ((W & 7) == 0) {
+    // W % 8 == 0: a chunk of 8 columns lies entirely inside or entirely outside the frame,
+    // and an outside chunk reads nothing (inner_value's fill for x >= W or y >= H)
+    uint4 v[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const int i = p * kThreads + t, r = i >> 4, k = i & 15;
+      const int y = qy + r, x = qx + 8 * k;
+      if (y < H && x + 8 <= W) {
+        v[p] = *reinterpret_cast<const uint4 *>(in + (size_t)y * W + x);
+      } else {
+        const short fv = !SEP ? -1 : ((RAD == 1 || y < H) ? 0 : -1);
+        invalid |= fv < 0;
+        const uint32_t f2 = (uint32_t)(uint16_t)fv * 0x10001u;
+        v[p] = make_uint4(f2, f2, f2, f2);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const int i = p * kThreads + t, r = i >> 4, k = i & 15;
+      *reinterpret_cast<uint4 *>(tile + (r + RAD) * kTWP + kCO + 8 * k) = v[p];
+    }
+  } else {
+    for (int i0 = t; i0 < 32 * 128; i0 += 8 * kThreads) {
+      short v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * kThreads, r = i >> 7, c = i & 127;
+        v[u] = inner_value<RAD, SEP>(in, qx + c, qy + r, W, H);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * kThreads, r = i >> 7, c = i & 127;
+        invalid |= v[u] < 0;
+        tile[(r + RAD) * kTWP + kCO + c] = v[u];
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NPH; p++) {
+    invalid |= hv[p] < 0;
+    tile[hidx[p]] = hv[p];
   }
   return invalid;
 }
@@ -248,17 +286,19 @@ __device__ __forceinline__ int sep_scale(int x, int y, int W, int H, int full, c
 }
 
 template <int RAD, bool FLOAT, bool SEP>
-__global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
+__global__ __launch_bounds__(kThreads * kTPW) void filter_kernel(FilterArgs a) {
   constexpr int KS = 2 * RAD + 1, TH = 32 + 2 * RAD, NR = 8 + 2 * RAD;
-  __shared__ __attribute__((aligned(16))) short tile[TH * kTWP];
+  __shared__ __attribute__((aligned(16))) short tiles[kTPW][TH * kTWP];
   const int W = a.width, H = a.height;
+  const int sub = kTPW > 1 ? (int)threadIdx.x / kThreads : 0;  // tile of this thread's 128-thread group
+  short *tile = tiles[sub];
   // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so workgroup b
   // takes tile (b % 8) * per + b / 8 -- each XCD walks a contiguous band of tiles and the
   // halo rows / columns it shares with its neighbours are fetched into its own L2.
   const int tiles_x = (W + 127) / 128, tiles_y = (H + 31) / 32, per_frame = tiles_x * tiles_y;
-  const int total = per_frame * a.nframes, per = (total + 7) / 8;
-  const int tid = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  if (tid >= total) return;
+  const int total = per_frame * a.nframes, units = (total + kTPW - 1) / kTPW, per = (units + 7) / 8;
+  const int tid = ((int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3)) * kTPW + sub;
+  if (tid >= total) return;  // whole waves leave (a barrier does not wait for ended waves)
   const int f = tid / per_frame, tr = tid - f * per_frame, ty = tr / tiles_x;
   const int qx = 128 * (tr - ty * tiles_x), qy = 32 * ty;
   const uint16_t *in = a.in + (size_t)f * W * H;
@@ -303,7 +343,7 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
     }
   }
 
-  const int c0 = 4 * (threadIdx.x & 31), r0 = 8 * (threadIdx.x >> 5);
+  const int c0 = 4 * (threadIdx.x & 31), r0 = 8 * ((threadIdx.x % kThreads) >> 5);
   const short *rowp = tile + r0 * kTWP + kCO - 2 + c0;
   // Horizontal sums are produced one row ahead of the vertical pass that consumes them
   // (a sliding window of KS rows stays live, not all NR: fewer VGPRs, higher occupancy).
@@ -376,7 +416,12 @@ __global__ __launch_bounds__(kThreads) void filter_kernel(FilterArgs a) {
     if (y >= H || x >= W) continue;
     uint16_t *o = out + (size_t)y * W + x;
     if ((W & 3) == 0 && x + 4 <= W) {
+#if MIP_FILTER_NT
+      typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store((v2u){res[0] | (res[1] << 16), res[2] | (res[3] << 16)}, reinterpret_cast<v2u *>(o));
+#else
       *reinterpret_cast<uint2 *>(o) = make_uint2(res[0] | (res[1] << 16), res[2] | (res[3] << 16));
+#endif
     } else {
 #pragma unroll
       for (int c = 0; c < 4; c++)
@@ -392,8 +437,9 @@ hipError_t launch_filter(const FilterArgs &a, hipStream_t s) {
   if (total > (1LL << 30) || (long long)(a.width + 256) * (a.height + 64) >= (1LL << 31) || a.width >= (1 << 22) ||
       a.height >= (1 << 22))
     return hipErrorInvalidValue;  // 32-bit / 24-bit index arithmetic in the gates
-  const dim3 grid((unsigned)((total + 7) / 8 * 8));
-  const dim3 block(kThreads);
+  const long long units = (total + kTPW - 1) / kTPW;
+  const dim3 grid((unsigned)((units + 7) / 8 * 8));
+  const dim3 block(kThreads * kTPW);
   switch (a.filter) {
     case 0: hipLaunchKernelGGL((filter_kernel<1, false, true>), grid, block, 0, s, a); break;
     case 1: hipLaunchKernelGGL((filter_kernel<1, true, true>), grid, block, 0, s, a); break;

@@ -871,9 +871,17 @@ __device__ __forceinline__ void tile_store(uint16_t *dst, int i, uint2 v) {
   *reinterpret_cast<uint2 *>(dst + row * kPitch + 4 * ch) = v;
 }
 
+// (whole workgroup, kWaves * 64 threads: every thread's loads are issued before its first
+// LDS store, so the workgroup waits for HBM once, not once per load; spare threads of the
+// last round repeat the last chunk -- same value, same LDS slot)
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
                                            int x0, int y0) {
-  for (int i = threadIdx.x; i < kTileLoads; i += blockDim.x) tile_store(dst, i, tile_load(frame, width, height, x0, y0, i));
+  constexpr int NT = 64 * kWaves, NL = (kTileLoads + NT - 1) / NT;
+  uint2 v[NL];
+#pragma unroll
+  for (int k = 0; k < NL; k++) v[k] = tile_load(frame, width, height, x0, y0, min((int)threadIdx.x + NT * k, kTileLoads - 1));
+#pragma unroll
+  for (int k = 0; k < NL; k++) tile_store(dst, min((int)threadIdx.x + NT * k, kTileLoads - 1), v[k]);
 }
 
 // Item = (frame, CTU, quadrant, slice) -> quadrant origin in the frame and frame index.
@@ -896,20 +904,35 @@ struct ItemPos {
 // Stage the reference lattice (ALT): rows 4i-1 (columns -4..63), columns 4i-1 (rows -1..63).
 __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
                                               int x0, int y0) {
-  constexpr int kChunks = kPitch / 4;
-  for (int i = threadIdx.x; i < 16 * kChunks; i += blockDim.x) {
-    const int row = i / kChunks, ch = i - row * kChunks;
+  // all loads first, then all LDS stores (as stage_tile)
+  constexpr int NT = 64 * kWaves, kChunks = kPitch / 4, NR = 16 * kChunks, NC = 16 * 65;
+  constexpr int NRL = (NR + NT - 1) / NT, NCL = (NC + NT - 1) / NT;
+  uint2 rv[NRL];
+  uint16_t cv[NCL];
+#pragma unroll
+  for (int k = 0; k < NRL; k++) {
+    const int i = min((int)threadIdx.x + NT * k, NR - 1), row = i / kChunks, ch = i - row * kChunks;
     const int fy = y0 + 4 * row - 1, fx = x0 - kColOff + 4 * ch;
-    uint2 v = make_uint2(0, 0);
+    rv[k] = make_uint2(0, 0);
     if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
-      v = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
-    *reinterpret_cast<uint2 *>(dst + row * kLatRowPitch + 4 * ch) = v;
+      rv[k] = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
+  }
+#pragma unroll
+  for (int k = 0; k < NCL; k++) {
+    const int i = min((int)threadIdx.x + NT * k, NC - 1), col = i / 65, yy = i - col * 65;
+    const int fy = y0 + yy - 1, fx = x0 + 4 * col - 1;
+    cv[k] = (fy >= 0 && fy < height && fx >= 0 && fx < width) ? frame[(size_t)fy * width + fx] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < NRL; k++) {
+    const int i = min((int)threadIdx.x + NT * k, NR - 1), row = i / kChunks, ch = i - row * kChunks;
+    *reinterpret_cast<uint2 *>(dst + row * kLatRowPitch + 4 * ch) = rv[k];
   }
   uint16_t *cols = dst + 16 * kLatRowPitch;
-  for (int i = threadIdx.x; i < 16 * 65; i += blockDim.x) {
-    const int col = i / 65, yy = i - col * 65;
-    const int fy = y0 + yy - 1, fx = x0 + 4 * col - 1;
-    cols[col * kLatColPitch + yy] = (fy >= 0 && fy < height && fx >= 0 && fx < width) ? frame[(size_t)fy * width + fx] : 0;
+#pragma unroll
+  for (int k = 0; k < NCL; k++) {
+    const int i = min((int)threadIdx.x + NT * k, NC - 1), col = i / 65, yy = i - col * 65;
+    cols[col * kLatColPitch + yy] = cv[k];
   }
 }
 
