@@ -62,10 +62,11 @@ def test_full_size_configs_vs_reference(gpu_available, name):
             assert G.sha(filt[f]) == fr["filtered_sha256"]
 
 
-@pytest.mark.parametrize("w,h", [(392, 136), (648, 232)])
+@pytest.mark.parametrize("w,h", [(392, 136), (648, 232), (300, 68), (292, 36)])
 @pytest.mark.parametrize("filt,nk", FILTERS)
 def test_filters_vs_oracle(gpu_available, filt, nk, w, h):
-    # partial tiles on both axes; 648x232 has 6 interior tiles (vectorised staging path)
+    # partial tiles on both axes; 648x232 has 6 interior tiles (vectorised staging path);
+    # widths 300 and 292 are not multiples of 8 (sample-by-sample staging)
     frame = synth_frame(w, h, 0x51, 1)
     # near-black samples: quotients around 1/2 (sum == scale/2 is the case where the
     # reference's fp32 division can fall just below the tie)
