@@ -75,3 +75,28 @@ def test_missing_library_fails_loudly(tmp_path):
     env = dict(os.environ, MIPGPU_LIB=str(tmp_path / "absent.so"))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert "MipError" in out.stdout and "no CPU fallback" in out.stdout, out.stdout + out.stderr
+
+
+def test_engine_create_rejects_bad_arguments_before_touching_the_gpu(lib):
+    """Argument checks in mip_engine_create run before any HIP call (safe without a GPU):
+    frame size, max_batch, best_k, and the per-launch CU count (2^31 - 256), which an 8K
+    batch of ~200 frames would overflow in int (mipgpu.cpp kMaxCus)."""
+    cases = [
+        ((1922, 1080, 1, 1), b"multiples of 4"),
+        ((0, 1080, 1, 1), b"multiples of 4"),
+        ((1920, 1080, 0, 1), b"max_batch"),
+        ((7680, 4320, 200, 1), b"CUs per launch"),
+        ((1920, 1080, 1, 33), b"best_k"),
+    ]
+    for (w, h, batch, k), msg in cases:
+        o = mipgpu._Opts()
+        lib.mip_opts_default(ctypes.byref(o))
+        o.max_batch, o.best_k = batch, k
+        e = ctypes.c_void_p()
+        assert lib.mip_engine_create(0, w, h, ctypes.byref(o), ctypes.byref(e)) != 0
+        assert not e.value
+        assert msg in lib.mip_last_error(), lib.mip_last_error()
+    # 195 frames of 8K fit (195 * 2040 * 5380 < 2^31 - 256); 196 do not
+    assert 195 * 2040 * 5380 <= (1 << 31) - 256 < 196 * 2040 * 5380
+    with pytest.raises(mipgpu.MipError, match="CUs per launch"):
+        mipgpu.MipEngine(7680, 4320, max_batch=196)
