@@ -227,6 +227,16 @@ static void cu_distortion(const uint16_t *orig, int width, int x, int y, int w, 
 
 /* ---------------------------------------------------------------------- search --- */
 
+/* Is the reference's cost of the CU at frame position (x, y) defined?  The reference reads
+ * samples by linear index y' * W + x' (intra.cl:100, 106, 236, 242, 718), so a CU right of
+ * the frame reads the next row's samples -- deterministic -- as long as every index stays
+ * below W * H.  The largest index a CU reads is its bottom-right original sample,
+ * (y + h - 1) * W + x + w - 1 (its reference row / column indexes are smaller).  CUs with
+ * y + h > H are skipped by initBoundaries (intra.cl:96-98, 232-234): stale LDS. */
+int mipo_cu_defined(int width, int height, int x, int y, int w, int h) {
+  return y + h < height || (y + h == height && x + w <= width);
+}
+
 static void search_ctu(const uint16_t *orig, const uint16_t *refs, int width, int height,
                        int ctu, int32_t *cost, int32_t *sad, int32_t *satd) {
   const int ctu_cols = (width + 127) / 128;
@@ -239,7 +249,7 @@ static void search_ctu(const uint16_t *orig, const uint16_t *refs, int width, in
       const int x = cx + axis_pos(sd->xb, sd->xs, sd->xd, cu % sd->ncols);
       const int y = cy + axis_pos(sd->yb, sd->ys, sd->yd, cu / sd->ncols);
       const size_t base = (size_t)ctu * MIP_COSTS_PER_CTU + sd->cost_offset + (size_t)cu * nm;
-      if (x + w > width || y + h > height) {
+      if (!mipo_cu_defined(width, height, x, y, w, h)) {
         for (int m = 0; m < nm; m++) {
           cost[base + m] = MIPO_UNAVAILABLE;
           if (sad) sad[base + m] = MIPO_UNAVAILABLE;
@@ -319,16 +329,39 @@ static float ref_fdiv(float v, int s) {
   return ldexpf(q, ev - es);
 }
 
-/* Validity of a tap at tile-relative (ty, tc) for the 2-D quarter-CTU kernels.  The
- * tile is 128x32 at (qx, qy); gates restate the halo fetch conditions:
- *   3x3: intra.cl:2903-2966, 5x5: intra.cl:3096-3189 (and the float twins).
- * Interior taps are valid when inside the frame (the reference only tests the row;
- * it assumes frame widths that are multiples of 128). */
-static int tap_valid(int ksz, int qx, int qy, int ty, int tc, int W, int H) {
+/* ---------------------------------------------------------- filter tiles ---
+ * Every filter kernel of the reference works on 128x32 quarter-CTU tiles, one work-group per
+ * tile (wg = ty * tiles_x + tx, intra.cl:2873-2879), and addresses the frame by LINEAR index
+ * (qy + r) * W + qx + c.  The oracle restates one tile at a time: tile_2d / tile_sep3 /
+ * tile_sep5 fill the tile's LDS the way the reference does and compute its 128 x rows
+ * outputs, each with a POISON flag = "depends on memory outside this frame" (a read at a
+ * linear index >= W * H: the next frame slot or the buffer's padding, never written for this
+ * frame).  filter_run then writes them like the reference (see there).
+ *
+ * LDS cell: value, or -1 for a cell the reference marks invalid, and the poison flag. */
+typedef struct {
+  int16_t v;
+  uint8_t p;
+} cell_t;
+
+/* Interior cell (ty, tc) of the tile at (qx, qy), read by linear index: right of the frame
+ * the index wraps into the next row (intra.cl:2905, 3098, 3331, 3597); past the frame end it
+ * is poison. */
+static cell_t interior_cell(const uint16_t *in, int W, int H, int qx, int qy, int ty, int tc) {
+  const long long idx = (long long)(qy + ty) * W + qx + tc;
+  cell_t c = {0, 0};
+  (void)H;
+  if (idx < (long long)W * H) c.v = (int16_t)in[idx];
+  else c.p = 1;
+  return c;
+}
+
+/* Halo gates of the 2-D quarter-CTU kernels: 3x3 intra.cl:2913-2966 (float twin 1696-1749),
+ * 5x5 intra.cl:3103-3189 (float twin 2372-2461).  (ty, tc) outside the 128x32 interior. */
+static int halo_valid_2d(int ksz, int qx, int qy, int ty, int tc, int W, int H) {
   const long long WH = (long long)W * H;
   const long long g = (long long)(qy + ty) * W + qx + tc;
   const int top = ty < 0, bot = ty >= 32, lft = tc < 0, rgt = tc >= 128;
-  if (!top && !bot && !lft && !rgt) return qy + ty < H && qx + tc < W;
   if ((top || bot) && (lft || rgt)) { /* corners */
     const int vy = top ? qy > 0 : qy + ty < H - 1;
     const int vx = lft ? qx > 0 : qx + tc < W - 1;
@@ -342,99 +375,117 @@ static int tap_valid(int ksz, int qx, int qy, int ty, int tc, int W, int H) {
   return g > 0 && g < WH && qx + tc > 0 && qx + tc < W - 1;
 }
 
-static void filter_2d(const uint16_t *in, uint16_t *out, int W, int H, const uint16_t *taps,
-                      int ksz, int is_float) {
-  const int rad = ksz / 2;
-  for (int y = 0; y < H; y++)
-    for (int x = 0; x < W; x++) {
-      const int qx = x & ~127, qy = y & ~31;
-      int sum = 0, scale = 0;
-      for (int dy = -rad; dy <= rad; dy++)
-        for (int dx = -rad; dx <= rad; dx++) {
-          const int c = taps[(dy + rad) * ksz + dx + rad];
-          if (!tap_valid(ksz, qx, qy, y - qy + dy, x - qx + dx, W, H)) continue;
-          sum += c * in[(size_t)(y + dy) * W + x + dx];
-          scale += c;
+static int round_div(int sum, int scale, int is_float) {
+  if (is_float) return (int)roundf(ref_fdiv((float)sum, scale)); /* intra.cl:1794, 2507 */
+  return (sum + scale / 2) / scale;                              /* intra.cl:3011, 3235 */
+}
+
+/* 2-D quarter-CTU kernels (intra.cl:2856, 1639, 3042, 2311): interior rows inside the frame
+ * are read (linear index), other interior rows are -1 (2904-2909); halo cells per the gates.
+ * Output = sum of c * v over the valid (>= 0) cells / sum of their c (2993-3011). */
+static void tile_2d(const uint16_t *in, int W, int H, int qx, int qy, const uint16_t *taps, int ksz,
+                    int is_float, int rows, int16_t *ov, uint8_t *op) {
+  enum { P = 132 };
+  static cell_t t[36 * P];
+  const int R = ksz / 2;
+  for (int ty = -R; ty < 32 + R; ty++)
+    for (int tc = -R; tc < 128 + R; tc++) {
+      cell_t c = {-1, 0};
+      if (ty >= 0 && ty < 32 && tc >= 0 && tc < 128) {
+        if (qy + ty < H) c = interior_cell(in, W, H, qx, qy, ty, tc);
+      } else if (halo_valid_2d(ksz, qx, qy, ty, tc, W, H)) {
+        c.v = (int16_t)in[(long long)(qy + ty) * W + qx + tc];
+      }
+      t[(ty + R) * P + tc + R] = c;
+    }
+  for (int r = 0; r < rows; r++)
+    for (int c = 0; c < 128; c++) {
+      int sum = 0, scale = 0, poison = 0;
+      for (int dy = -R; dy <= R; dy++)
+        for (int dx = -R; dx <= R; dx++) {
+          const cell_t e = t[(r + dy + R) * P + c + dx + R];
+          const int k = taps[(dy + R) * ksz + dx + R];
+          poison |= e.p;
+          if (e.p || e.v < 0) continue;
+          sum += k * e.v;
+          scale += k;
         }
-      int v;
-      if (is_float) v = (int)roundf(ref_fdiv((float)sum, scale)); /* intra.cl:1794, 2507 */
-      else v = (sum + scale / 2) / scale;                         /* intra.cl:3011, 3235 */
-      out[(size_t)y * W + x] = (uint16_t)v;
+      ov[r * 128 + c] = poison ? 0 : (int16_t)round_div(sum, scale, is_float);
+      op[r * 128 + c] = (uint8_t)poison;
     }
 }
 
-/* ------------------------------------------------------- separable (1-D) filters ---
- * filterFrame_1d_{int,float} (intra.cl:3267, 1828) and filterFrame_1d_{int,float}_5x5
- * (intra.cl:3508, 2539), restated per 128x32 quarter-CTU tile:
+/* Separable 3-tap kernels filterFrame_1d_{int,float} (intra.cl:3267, 1828):
  *  - taps t = row 0 of the 2-D kernel, applied horizontally and then vertically;
- *  - the tile (+1 / +2 sample halo) is gathered with the reference's own fetch conditions
- *    (including the ones stricter than "inside the frame": right halo columns need
- *    x < W-1, bottom halo rows / corners need y < H-1 resp. H-2, see below); samples
- *    that are not fetched count as 0 (3-tap) or are dropped (5-tap: marker -1 -> 0);
- *    interior samples below the frame (3-tap tiles read them unguarded, intra.cl:3330)
- *    are taken as 0, which is what the reference reads from zeroed padding; so are
- *    interior samples right of the frame (W % 128 != 0, where the reference's linear
- *    index would wrap -- documented deviation), while halo rows keep the reference's
- *    linear-index reads;
- *  - 3-tap scale: (2+t1)^2 inside, (1+t1)(2+t1) on a frame edge row/column, (1+t1)^2 in
- *    a corner (t0 = t2 = 1 for every kernel of the library) (intra.cl:3281-3285);
- *  - 5-tap: horizontal sums only for tile rows inside the frame; vertical: each invalid
- *    row drops its tap weight from the 2-D full scale, then position classes (outer /
- *    inner edge rows and columns, corners, "interface") select 2-D sub-sums of the 5x5
- *    kernel as the scale (intra.cl:3523-3557, 3745-3790);
+ *  - LDS zeroed (3311-3320), interior fetched UNGUARDED (3330-3332: rows below the frame
+ *    read past its end -> poison), halo rows / columns / corners with the gates 3336-3366
+ *    (unfetched halo cells stay 0);
+ *  - horizontal pass over all 34 rows (3377-3405), vertical pass (3418-3478) with the
+ *    closed-form scales: (2+t1)^2 inside, (1+t1)(2+t1) on a frame edge row / column,
+ *    (1+t1)^2 in a corner (t0 = t2 = 1 for every kernel of the library) (3281-3285);
  *  - rounding: int (v + s/2)/s, float round(v/s) on float operands. */
-static void filter_1d_tile3(const uint16_t *in, uint16_t *out, int W, int H, int X, int Y,
-                            const uint16_t *taps, int is_float) {
+static void tile_sep3(const uint16_t *in, int W, int H, int X, int Y, const uint16_t *taps, int is_float,
+                      int rows, int16_t *ov, uint8_t *op) {
   enum { P = 130, R = 34 };
-  static int16_t tile[R * P];
+  static cell_t tile[R * P];
   static double hp[R * P];
+  static uint8_t hpp[R * P];
   const int t0 = taps[0], t1 = taps[1], t2 = taps[2];
   memset(tile, 0, sizeof tile);
   for (int r = 0; r < 32; r++)
-    for (int c = 0; c < 128; c++) {  /* unguarded interior fetch: outside the frame -> 0 */
-      const int y = Y + r, x = X + c;
-      tile[(r + 1) * P + c + 1] = (y < H && x < W) ? (int16_t)in[(size_t)y * W + x] : 0;
-    }
+    for (int c = 0; c < 128; c++) tile[(r + 1) * P + c + 1] = interior_cell(in, W, H, X, Y, r, c);
   const long long WH = (long long)W * H;
   for (int side = 0; side < 2; side++)  /* top (row Y-1) and bottom (row Y+32) halo rows */
     for (int c = 0; c < 128; c++) {
       const long long idx = (long long)(Y - 1 + 33 * side) * W + X + c;
-      if (idx > 0 && idx < WH) tile[(33 * side) * P + 1 + c] = (int16_t)in[idx];
+      if (idx > 0 && idx < WH) tile[(33 * side) * P + 1 + c].v = (int16_t)in[idx];
     }
   for (int r = 1; r <= 32; r++)       /* left (X-1) and right (X+128) halo columns */
     for (int side = 0; side < 2; side++) {
       const long long idx = (long long)(Y + r - 1) * W + X - 1 + 129 * side;
-      if (idx > 0 && idx < WH && X + side > 0 && X + 129 * side < W - 1) tile[r * P + 129 * side] = (int16_t)in[idx];
+      if (idx > 0 && idx < WH && X + side > 0 && X + 129 * side < W - 1) tile[r * P + 129 * side].v = (int16_t)in[idx];
     }
   const long long b = (long long)Y * W + X;
-  if (b - W - 1 > 0 && X > 0 && Y > 0) tile[0] = (int16_t)in[b - W - 1];
-  if (b - W + 128 > 0 && X + 128 < W - 1 && Y > 0) tile[129] = (int16_t)in[b - W + 128];
-  if (b + 32LL * W - 1 < WH && X > 0 && Y + 32 < H - 1) tile[33 * P] = (int16_t)in[b + 32LL * W - 1];
-  if (b + 32LL * W + 128 < WH && X + 128 < W - 1 && Y + 32 < H - 1) tile[33 * P + 129] = (int16_t)in[b + 32LL * W + 128];
+  if (b - W - 1 > 0 && X > 0 && Y > 0) tile[0].v = (int16_t)in[b - W - 1];
+  if (b - W + 128 > 0 && X + 128 < W - 1 && Y > 0) tile[129].v = (int16_t)in[b - W + 128];
+  if (b + 32LL * W - 1 < WH && X > 0 && Y + 32 < H - 1) tile[33 * P].v = (int16_t)in[b + 32LL * W - 1];
+  if (b + 32LL * W + 128 < WH && X + 128 < W - 1 && Y + 32 < H - 1) tile[33 * P + 129].v = (int16_t)in[b + 32LL * W + 128];
   for (int r = 0; r < R; r++)         /* horizontal pass (halo rows included) */
-    for (int c = 1; c <= 128; c++)
-      hp[r * P + c] = (double)tile[r * P + c - 1] * t0 + (double)tile[r * P + c] * t1 + (double)tile[r * P + c + 1] * t2;
+    for (int c = 1; c <= 128; c++) {
+      const cell_t *e = tile + r * P + c;
+      hp[r * P + c] = (double)e[-1].v * t0 + (double)e[0].v * t1 + (double)e[1].v * t2;
+      hpp[r * P + c] = e[-1].p | e[0].p | e[1].p;
+    }
   const int full = 4 * t0 + 4 * t1 + t1 * t1, corner = t0 + 2 * t1 + t1 * t1, edge = 2 * t0 + 3 * t1 + t1 * t1;
-  const int rows = H - Y < 32 ? H - Y : 32;
   for (int r = 0; r < rows; r++)
-    for (int c = 0; c < 128 && X + c < W; c++) {
+    for (int c = 0; c < 128; c++) {
       const int y = Y + r, x = X + c;
       const int nb = (y == 0) + (y == H - 1) + (x == 0) + (x == W - 1);
       const int sc = nb >= 2 ? corner : (nb ? edge : full);
       const int k = (r + 1) * P + c + 1;
       const double v = hp[k - P] * t0 + hp[k] * t1 + hp[k + P] * t2;
+      const int poison = hpp[k - P] | hpp[k] | hpp[k + P];
       int res;
       if (is_float) res = (int)roundf(ref_fdiv((float)v, sc));
       else res = ((int)v + sc / 2) / sc;
-      out[(size_t)y * W + x] = (uint16_t)res;
+      ov[r * 128 + c] = poison ? 0 : (int16_t)res;
+      op[r * 128 + c] = (uint8_t)poison;
     }
 }
 
-static void filter_1d_tile5(const uint16_t *in, uint16_t *out, int W, int H, int X, int Y,
-                            const uint16_t *k2d, int is_float) {
+/* Separable 5-tap kernels filterFrame_1d_{int,float}_5x5 (intra.cl:3508, 2539):
+ *  - LDS filled with -1 (3576-3585), interior rows inside the frame fetched (3595-3598),
+ *    halo per the gates 3606-3688;
+ *  - horizontal pass only for tile rows that are frame rows (3705-3726), -1 cells count 0;
+ *  - vertical pass: each row without a horizontal pass drops its tap weight from the 2-D full
+ *    scale, then the position classes (outer / inner edge rows and columns, corners,
+ *    "interface") select 2-D sub-sums of the 5x5 kernel as the scale (3523-3557, 3749-3788). */
+static void tile_sep5(const uint16_t *in, int W, int H, int X, int Y, const uint16_t *k2d, int is_float,
+                      int rows, int16_t *ov, uint8_t *op) {
   enum { P = 132, R = 36 };
-  static int16_t tile[R * P];
+  static cell_t tile[R * P];
   static double hp[R * P];
+  static uint8_t hpp[R * P];
   static int hv[R];
   const uint16_t *t = k2d; /* row 0 */
   int full = 0, oc = 0, ic = 0, itf = 0, oe = 0, ie = 0;
@@ -448,79 +499,85 @@ static void filter_1d_tile5(const uint16_t *in, uint16_t *out, int W, int H, int
       if (j >= 2) oe += v;
       if (j >= 1) ie += v;
     }
-  for (int i = 0; i < R * P; i++) tile[i] = -1;
+  for (int i = 0; i < R * P; i++) tile[i] = (cell_t){-1, 0};
   const long long WH = (long long)W * H, b = (long long)Y * W + X;
   for (int r = 0; r < 32; r++)
     if (Y + r < H)
-      for (int c = 0; c < 128; c++) tile[(r + 2) * P + c + 2] = X + c < W ? (int16_t)in[(size_t)(Y + r) * W + X + c] : 0;
+      for (int c = 0; c < 128; c++) tile[(r + 2) * P + c + 2] = interior_cell(in, W, H, X, Y, r, c);
   for (int r = 0; r < 2; r++)         /* top halo rows Y-2, Y-1 */
     for (int c = 0; c < 128; c++) {
       const long long idx = b - 2LL * W + (long long)r * W + c;
-      if (idx > 0 && idx < WH && Y > 0) tile[r * P + 2 + c] = (int16_t)in[idx];
+      if (idx > 0 && idx < WH && Y > 0) tile[r * P + 2 + c].v = (int16_t)in[idx];
     }
   for (int r = 34; r < 36; r++)       /* bottom halo rows Y+32, Y+33: need Y + r < H - 1 */
     for (int c = 0; c < 128; c++) {
       const long long idx = b - 2LL * W + (long long)r * W + c;
-      if (idx > 0 && idx < WH && Y + r < H - 1) tile[r * P + 2 + c] = (int16_t)in[idx];
+      if (idx > 0 && idx < WH && Y + r < H - 1) tile[r * P + 2 + c].v = (int16_t)in[idx];
     }
   for (int r = 0; r < 32; r++)        /* side halo columns X-2, X-1, X+128, X+129 */
     for (int q = 0; q < 4; q++) {
       const int c = q < 2 ? q : q + 128;
       const long long idx = b - 2 + (long long)r * W + c;
-      if (idx > 0 && idx < WH && X - 2 + c > 0 && X - 2 + c < W - 1) tile[(2 + r) * P + c] = (int16_t)in[idx];
+      if (idx > 0 && idx < WH && X - 2 + c > 0 && X - 2 + c < W - 1) tile[(2 + r) * P + c].v = (int16_t)in[idx];
     }
   if (X > 0 && Y > 0) {
-    tile[0] = (int16_t)in[b - 2 * W - 2];
-    tile[1] = (int16_t)in[b - 2 * W - 1];
-    tile[P] = (int16_t)in[b - W - 2];
-    tile[P + 1] = (int16_t)in[b - W - 1];
+    tile[0].v = (int16_t)in[b - 2 * W - 2];
+    tile[1].v = (int16_t)in[b - 2 * W - 1];
+    tile[P].v = (int16_t)in[b - W - 2];
+    tile[P + 1].v = (int16_t)in[b - W - 1];
   }
   if (Y > 0) {
     if (X + 128 < W - 1) {
-      tile[P - 2] = (int16_t)in[b - 2 * W + 128];
-      tile[2 * P - 2] = (int16_t)in[b - W + 128];
+      tile[P - 2].v = (int16_t)in[b - 2 * W + 128];
+      tile[2 * P - 2].v = (int16_t)in[b - W + 128];
     }
     if (X + 129 < W - 1) {
-      tile[P - 1] = (int16_t)in[b - 2 * W + 129];
-      tile[2 * P - 1] = (int16_t)in[b - W + 129];
+      tile[P - 1].v = (int16_t)in[b - 2 * W + 129];
+      tile[2 * P - 1].v = (int16_t)in[b - W + 129];
     }
   }
   if (X > 0) {
     if (Y + 32 < H - 1) {
-      tile[34 * P] = (int16_t)in[b + 32LL * W - 2];
-      tile[34 * P + 1] = (int16_t)in[b + 32LL * W - 1];
+      tile[34 * P].v = (int16_t)in[b + 32LL * W - 2];
+      tile[34 * P + 1].v = (int16_t)in[b + 32LL * W - 1];
     }
     if (Y + 33 < H - 1) {
-      tile[35 * P] = (int16_t)in[b + 33LL * W - 2];
-      tile[35 * P + 1] = (int16_t)in[b + 33LL * W - 1];
+      tile[35 * P].v = (int16_t)in[b + 33LL * W - 2];
+      tile[35 * P + 1].v = (int16_t)in[b + 33LL * W - 1];
     }
   }
-  if (Y + 32 < H - 1 && X + 129 < W - 1) tile[35 * P - 1] = (int16_t)in[b + 32LL * W + 129];
-  if (Y + 32 < H - 1 && X + 128 < W - 1) tile[35 * P - 2] = (int16_t)in[b + 32LL * W + 128];
-  if (Y + 33 < H - 1 && X + 129 < W - 1) tile[36 * P - 1] = (int16_t)in[b + 33LL * W + 129];
-  if (Y + 33 < H - 1 && X + 128 < W - 1) tile[36 * P - 2] = (int16_t)in[b + 33LL * W + 128];
+  if (Y + 32 < H - 1 && X + 129 < W - 1) tile[35 * P - 1].v = (int16_t)in[b + 32LL * W + 129];
+  if (Y + 32 < H - 1 && X + 128 < W - 1) tile[35 * P - 2].v = (int16_t)in[b + 32LL * W + 128];
+  if (Y + 33 < H - 1 && X + 129 < W - 1) tile[36 * P - 1].v = (int16_t)in[b + 33LL * W + 129];
+  if (Y + 33 < H - 1 && X + 128 < W - 1) tile[36 * P - 2].v = (int16_t)in[b + 33LL * W + 128];
   for (int r = 0; r < R; r++) {       /* horizontal pass: tile rows that are frame rows */
     hv[r] = Y + r - 2 >= 0 && Y + r - 2 < H;
     if (!hv[r]) continue;
     for (int c = 2; c < 130; c++) {
       double acc = 0;
+      uint8_t p = 0;
       for (int d = -2; d <= 2; d++) {
-        const int v = tile[r * P + c + d];
-        acc += (double)(v < 0 ? 0 : v) * t[2 + d];
+        const cell_t e = tile[r * P + c + d];
+        acc += (double)(e.v < 0 ? 0 : e.v) * t[2 + d];
+        p |= e.p;
       }
       hp[r * P + c] = acc;
+      hpp[r * P + c] = p;
     }
   }
-  const int rows = H - Y < 32 ? H - Y : 32;
   for (int r = 0; r < rows; r++)
-    for (int c = 0; c < 128 && X + c < W; c++) {
+    for (int c = 0; c < 128; c++) {
       const int y = Y + r, x = X + c;
-      int sc = full;
+      int sc = full, poison = 0;
       double v = 0;
       for (int d = -2; d <= 2; d++) {
         const int rr = r + 2 + d;
-        if (!hv[rr]) sc -= t[2 + d];
-        else v += hp[rr * P + c + 2] * t[2 + d];
+        if (!hv[rr]) {
+          sc -= t[2 + d];
+        } else {
+          v += hp[rr * P + c + 2] * t[2 + d];
+          poison |= hpp[rr * P + c + 2];
+        }
       }
       const int otb = y == 0 || y == H - 1, itb = y == 1 || y == H - 2;
       const int olr = x == 0 || x == W - 1, ilr = x == 1 || x == W - 2;
@@ -536,44 +593,96 @@ static void filter_1d_tile5(const uint16_t *in, uint16_t *out, int W, int H, int
       int res;
       if (is_float) res = (int)roundf(ref_fdiv((float)v, sc));
       else res = ((int)v + sc / 2) / sc;
-      out[(size_t)y * W + x] = (uint16_t)res;
+      ov[r * 128 + c] = poison ? 0 : (int16_t)res;
+      op[r * 128 + c] = (uint8_t)poison;
     }
 }
 
-static void filter_1d(const uint16_t *in, uint16_t *out, int W, int H, int kernel_idx, int five, int is_float) {
-  for (int Y = 0; Y < H; Y += 32)
-    for (int X = 0; X < W; X += 128) {
-      if (five) filter_1d_tile5(in, out, W, H, X, Y, TAPS5 + 25 * kernel_idx, is_float);
-      else filter_1d_tile3(in, out, W, H, X, Y, TAPS3 + 9 * kernel_idx, is_float);
-    }
+/* Run a filter over the frame and write its outputs the way the reference does: every tile
+ * stores all 128 columns of its min(32, H - qy) rows by linear index (intra.cl:3027-3038,
+ * 3489-3505).  Samples x < W get their OWNING tile's value.  At widths that are not multiples
+ * of 128 the last tile column also stores its columns c >= W - qx, which land on the next
+ * row, over samples another work-group writes: the two stores race.  Where both values
+ * agree the sample is well defined; where they differ (or either is poison) the reference's
+ * result depends on the work-groups' timing and the sample is marked undefined.  `undef`
+ * (may be NULL) receives 1 for undefined samples (poison or race). */
+static int filter_run(const uint16_t *in, uint16_t *out, uint8_t *undef, int W, int H, int filter, int kernel_idx) {
+  const int five = filter >= MIPO_FILTER_1D_INT_5x5;
+  const int sep = filter == MIPO_FILTER_1D_INT || filter == MIPO_FILTER_1D_FLOAT || filter == MIPO_FILTER_1D_INT_5x5 ||
+                  filter == MIPO_FILTER_1D_FLOAT_5x5;
+  const int is_float = filter == MIPO_FILTER_1D_FLOAT || filter == MIPO_FILTER_2D_FLOAT ||
+                       filter == MIPO_FILTER_1D_FLOAT_5x5 || filter == MIPO_FILTER_2D_FLOAT_5x5;
+  if (kernel_idx < 0 || kernel_idx >= (five ? 3 : 5)) return -1;
+  const uint16_t *taps = five ? TAPS5 + 25 * kernel_idx : TAPS3 + 9 * kernel_idx;
+  static int16_t ov[32 * 128];
+  static uint8_t op[32 * 128];
+  const long long WH = (long long)W * H;
+  uint8_t *und = undef ? undef : (uint8_t *)malloc((size_t)WH);
+  if (!und) return -1;
+  const int tiles_x = (W + 127) / 128, qx_last = 128 * (tiles_x - 1);
+  for (int pass = 0; pass < 2; pass++) /* 0: owning stores, 1: the wrapped stores */
+    for (int qy = 0; qy < H; qy += 32)
+      for (int qx = pass ? qx_last : 0; qx < W; qx += 128) {
+        if (pass && W - qx >= 128) continue;
+        const int rows = H - qy < 32 ? H - qy : 32;
+        if (!sep) tile_2d(in, W, H, qx, qy, taps, five ? 5 : 3, is_float, rows, ov, op);
+        else if (five) tile_sep5(in, W, H, qx, qy, taps, is_float, rows, ov, op);
+        else tile_sep3(in, W, H, qx, qy, taps, is_float, rows, ov, op);
+        for (int r = 0; r < rows; r++)
+          for (int c = pass ? W - qx : 0; c < (pass ? 128 : (W - qx < 128 ? W - qx : 128)); c++) {
+            const long long idx = (long long)(qy + r) * W + qx + c;
+            if (idx >= WH) continue; /* past the frame: the next slot / padding */
+            const uint16_t v = (uint16_t)ov[r * 128 + c];
+            if (!pass) {
+              out[idx] = v;
+              und[idx] = op[r * 128 + c];
+            } else if (op[r * 128 + c] || v != out[idx]) {
+              und[idx] = 1;
+            }
+          }
+      }
+  if (!undef) free(und);
+  return 0;
 }
 
-int mipo_filter_frame(const uint16_t *in, uint16_t *out, int width, int height, int filter,
-                      int kernel_idx) {
-  switch (filter) {
-    case MIPO_FILTER_1D_INT:
-    case MIPO_FILTER_1D_FLOAT:
-      if (kernel_idx < 0 || kernel_idx >= 5) return -1;
-      filter_1d(in, out, width, height, kernel_idx, 0, filter == MIPO_FILTER_1D_FLOAT);
-      return 0;
-    case MIPO_FILTER_1D_INT_5x5:
-    case MIPO_FILTER_1D_FLOAT_5x5:
-      if (kernel_idx < 0 || kernel_idx >= 3) return -1;
-      filter_1d(in, out, width, height, kernel_idx, 1, filter == MIPO_FILTER_1D_FLOAT_5x5);
-      return 0;
-    case MIPO_FILTER_2D_INT:
-    case MIPO_FILTER_2D_FLOAT:
-      if (kernel_idx < 0 || kernel_idx >= 5) return -1;
-      filter_2d(in, out, width, height, TAPS3 + 9 * kernel_idx, 3, filter == MIPO_FILTER_2D_FLOAT);
-      return 0;
-    case MIPO_FILTER_2D_INT_5x5:
-    case MIPO_FILTER_2D_FLOAT_5x5:
-      if (kernel_idx < 0 || kernel_idx >= 3) return -1;
-      filter_2d(in, out, width, height, TAPS5 + 25 * kernel_idx, 5,
-                filter == MIPO_FILTER_2D_FLOAT_5x5);
-      return 0;
-    default:
-      return -1;
+int mipo_filter_frame_ex(const uint16_t *in, uint16_t *out, uint8_t *undef, int width, int height, int filter,
+                         int kernel_idx) {
+  if (filter < 0 || filter > 7) return -1;
+  return filter_run(in, out, undef, width, height, filter, kernel_idx);
+}
+
+int mipo_filter_frame(const uint16_t *in, uint16_t *out, int width, int height, int filter, int kernel_idx) {
+  return mipo_filter_frame_ex(in, out, NULL, width, height, filter, kernel_idx);
+}
+
+/* CUs whose reference samples (read from a filtered frame, see mipo_cu_boundaries) include
+ * an undefined sample of that frame (mipo_filter_frame_ex): 1 per CU in CU order
+ * ctu*5380 + shape CU prefix + cu.  CUs the search itself leaves unavailable are not
+ * marked. */
+void mipo_ref_undefined_cus(const uint8_t *undef, int width, int height, uint8_t *cu_out) {
+  const int ctu_cols = (width + 127) / 128, n = mipo_num_ctus(width, height);
+  size_t k = 0;
+  for (int ctu = 0; ctu < n; ctu++) {
+    const int cx = 128 * (ctu % ctu_cols), cy = 128 * (ctu / ctu_cols);
+    for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+      const mip_shape_desc *sd = &SHAPES[s];
+      for (int cu = 0; cu < sd->ncu; cu++, k++) {
+        const int x = cx + axis_pos(sd->xb, sd->xs, sd->xd, cu % sd->ncols);
+        const int y = cy + axis_pos(sd->yb, sd->ys, sd->yd, cu / sd->ncols);
+        int bad = 0;
+        if (mipo_cu_defined(width, height, x, y, sd->w, sd->h)) {
+          if (y > 0)
+            for (int i = 0; i < sd->w; i++) bad |= undef[(size_t)(y - 1) * width + x + i];
+          else if (x > 0)
+            bad |= undef[x - 1];
+          if (x > 0)
+            for (int i = 0; i < sd->h; i++) bad |= undef[(size_t)(y + i) * width + x - 1];
+          else if (y > 0)
+            bad |= undef[(size_t)(y - 1) * width];
+        }
+        cu_out[k] = (uint8_t)bad;
+      }
+    }
   }
 }
 

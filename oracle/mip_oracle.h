@@ -39,7 +39,7 @@ int64_t mipo_costs_per_frame(int width, int height);
  * are taken from (== orig for USE_ALTERNATIVE_SAMPLES=0, the filtered frame otherwise).
  * Outputs use the reference cost layout ALL_stridedDistortionsPerCtu (constants.h:1558):
  * index = ctu*97840 + shape.cost_offset + cu*2*modes + mode.  sad/satd may be NULL.
- * CUs that do not lie completely inside the frame get MIPO_UNAVAILABLE.
+ * CUs whose cost the reference leaves undefined (mipo_cu_defined) get MIPO_UNAVAILABLE.
  * nthreads<=0: all OpenMP threads. */
 void mipo_search_frame(const uint16_t *orig, const uint16_t *refs, int width, int height,
                        int32_t *cost, int32_t *sad, int32_t *satd, int nthreads);
@@ -67,6 +67,21 @@ void mipo_clip_counts(long long *out, int reset);
 
 int mipo_filter_frame(const uint16_t *in, uint16_t *out, int width, int height,
                       int filter, int kernel_idx);
+
+/* Same, plus undef[i] = 1 for samples the reference leaves undefined: they depend on memory
+ * past the frame's end (the separable filters' unguarded interior rows, intra.cl:3330; the
+ * wrapped columns of the last tile column in the last rows) or on the order of two
+ * work-groups' stores (the last tile column's wrapped stores at widths that are not
+ * multiples of 128).  Defined samples are the reference's own output bit for bit. */
+int mipo_filter_frame_ex(const uint16_t *in, uint16_t *out, uint8_t *undef, int width, int height,
+                         int filter, int kernel_idx);
+
+/* 1 = the reference defines the cost of the CU at frame position (x, y) of size w x h. */
+int mipo_cu_defined(int width, int height, int x, int y, int w, int h);
+
+/* Per CU (CU order ctu*5380 + shape prefix + cu): 1 if the CU is defined but one of its
+ * reference samples is an undefined sample of the filtered frame. */
+void mipo_ref_undefined_cus(const uint8_t *undef, int width, int height, uint8_t *cu_out);
 
 /* Synthetic 10-bit frames: kind 0 = structured, 1 = uniform noise. */
 void mipo_synth_frame(uint16_t *out, int width, int height, uint64_t seed, int kind);

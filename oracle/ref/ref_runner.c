@@ -14,7 +14,13 @@
  * usage: ref_runner --bins DIR --width W --height H [--frames N] [--synth KIND:SEED]
  *                   [--input FILE.u16] [--filter NAME] [--kernel-idx K] [--full-dist]
  *                   [--out-cost F] [--out-sad F] [--out-satd F] [--out-filtered F]
- *                   [--reps R]
+ *                   [--reps R] [--fill V]
+ *
+ * --fill V: every device buffer (frame slots and their padding, filtered frames, the
+ * boundary / prediction scratch, the cost tables) starts as the 16-bit pattern V instead
+ * of zero.  Outputs that change with V depend on memory the reference never wrote for
+ * this frame (out-of-frame reads, stale scratch): tools/ref_fill_experiment.py runs the
+ * reference with two fill values to find them.
  */
 #define CL_TARGET_OPENCL_VERSION 120
 #include <CL/cl.h>
@@ -105,7 +111,7 @@ static void write_file(const char *path, const void *data, size_t bytes) {
 int main(int argc, char **argv) {
   const char *bins = "oracle/_ref", *input = NULL, *filter = NULL;
   const char *out_cost = NULL, *out_sad = NULL, *out_satd = NULL, *out_filt = NULL;
-  int W = 0, H = 0, frames = 1, kidx = 0, full = 0, reps = 1, kind = 0;
+  int W = 0, H = 0, frames = 1, kidx = 0, full = 0, reps = 1, kind = 0, fill = 0;
   unsigned long long seed = 0x1080;
   for (int i = 1; i < argc; i++) {
     const char *a = argv[i], *v = i + 1 < argc ? argv[i + 1] : "";
@@ -123,6 +129,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(a, "--out-satd")) out_satd = v, i++;
     else if (!strcmp(a, "--out-filtered")) out_filt = v, i++;
     else if (!strcmp(a, "--reps")) reps = atoi(v), i++;
+    else if (!strcmp(a, "--fill")) fill = (int)strtol(v, NULL, 0), i++;
     else { fprintf(stderr, "unknown argument %s\n", a); return 2; }
   }
   if (W <= 0 || H <= 0 || frames <= 0) { fprintf(stderr, "need --width/--height\n"); return 2; }
@@ -166,14 +173,13 @@ int main(int argc, char **argv) {
   const size_t pad = (size_t)W * 256 + 4096;
   cl_mem m_ref = clCreateBuffer(ctx, CL_MEM_READ_WRITE, (slots * fs + pad) * 2, NULL, &err); CHECK(err, "buf");
   cl_mem m_filt = clCreateBuffer(ctx, CL_MEM_READ_WRITE, (slots * fs + pad) * 2, NULL, &err); CHECK(err, "buf");
-  /* Zero both frame buffers: the separable filters read rows below the frame unguarded
-   * (intra.cl:3330-3332); with zeros there they compute the in-frame filter. */
-  {
-    const cl_short zero = 0;
-    CHECK(clEnqueueFillBuffer(q, m_ref, &zero, sizeof zero, 0, (slots * fs + pad) * 2, 0, NULL, NULL), "fill");
-    CHECK(clEnqueueFillBuffer(q, m_filt, &zero, sizeof zero, 0, (slots * fs + pad) * 2, 0, NULL, NULL), "fill");
-    CHECK(clFinish(q), "fill finish");
-  }
+  /* Both frame buffers start as the fill pattern (zero by default): the separable filters
+   * read rows below the frame unguarded (intra.cl:3330-3332), and at widths that are not
+   * multiples of 128 the linear indexes of the last CTU / tile column run past the frame
+   * end (intra.cl:100, 718, 2905); with --fill those reads see V. */
+  const cl_short fillv = (cl_short)fill;
+  CHECK(clEnqueueFillBuffer(q, m_ref, &fillv, sizeof fillv, 0, (slots * fs + pad) * 2, 0, NULL, NULL), "fill");
+  CHECK(clEnqueueFillBuffer(q, m_filt, &fillv, sizeof fillv, 0, (slots * fs + pad) * 2, 0, NULL, NULL), "fill");
   cl_mem m_redT = clCreateBuffer(ctx, CL_MEM_READ_WRITE, slots * nctus * RED_PER_CTU * 2, NULL, &err); CHECK(err, "buf");
   cl_mem m_redL = clCreateBuffer(ctx, CL_MEM_READ_WRITE, slots * nctus * RED_PER_CTU * 2, NULL, &err); CHECK(err, "buf");
   cl_mem m_refT = clCreateBuffer(ctx, CL_MEM_READ_WRITE, slots * nctus * REF_PER_CTU * 2, NULL, &err); CHECK(err, "buf");
@@ -183,6 +189,15 @@ int main(int argc, char **argv) {
   cl_mem m_min = clCreateBuffer(ctx, CL_MEM_READ_WRITE, cost_bytes, NULL, &err); CHECK(err, "buf");
   cl_mem m_sad = clCreateBuffer(ctx, CL_MEM_READ_WRITE, cost_bytes, NULL, &err); CHECK(err, "buf");
   cl_mem m_satd = clCreateBuffer(ctx, CL_MEM_READ_WRITE, cost_bytes, NULL, &err); CHECK(err, "buf");
+  {
+    cl_mem scratch[] = {m_redT, m_redL, m_refT, m_refL, m_pred, m_min, m_sad, m_satd};
+    size_t bytes[] = {slots * nctus * RED_PER_CTU * 2, slots * nctus * RED_PER_CTU * 2, slots * nctus * REF_PER_CTU * 2,
+                      slots * nctus * REF_PER_CTU * 2, slots * (size_t)nctus * PRED_PER_CTU * 2, cost_bytes, cost_bytes,
+                      cost_bytes};
+    for (int b = 0; b < 8; b++)
+      CHECK(clEnqueueFillBuffer(q, scratch[b], &fillv, sizeof fillv, 0, bytes[b], 0, NULL, NULL), "fill scratch");
+    CHECK(clFinish(q), "fill finish");
+  }
 
   cl_kernel k_filt = NULL;
   if (filter) { k_filt = clCreateKernel(p2, filter, &err); CHECK(err, "filter kernel"); }

@@ -31,6 +31,10 @@ def lib():
                                        i32p, i32p, i32p, ctypes.c_int]
         L.mipo_filter_frame.argtypes = [u16p, u16p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.mipo_filter_frame.restype = ctypes.c_int
+        u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+        L.mipo_filter_frame_ex.argtypes = [u16p, u16p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.mipo_filter_frame_ex.restype = ctypes.c_int
+        L.mipo_ref_undefined_cus.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
         L.mipo_synth_frame.argtypes = [u16p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
         L.mipo_num_ctus.argtypes = [ctypes.c_int, ctypes.c_int]
         L.mipo_num_ctus.restype = ctypes.c_int
@@ -65,13 +69,30 @@ def clip_counts(reset=True):
     return int(out[0]), int(out[1])
 
 
-def filter_frame(frame, filter_name, kernel_idx):
+def filter_frame(frame, filter_name, kernel_idx, with_undefined=False):
+    """Oracle filter.  with_undefined: also return the bool mask of samples the reference
+    leaves undefined (reads past the frame end, racing stores; mipo_filter_frame_ex)."""
     frame = np.ascontiguousarray(frame, np.uint16)
     out = np.zeros_like(frame)
-    rc = lib().mipo_filter_frame(frame, out, frame.shape[1], frame.shape[0], FILTERS.index(filter_name), kernel_idx)
+    und = np.zeros(frame.shape, np.uint8)
+    rc = lib().mipo_filter_frame_ex(frame, out, und, frame.shape[1], frame.shape[0], FILTERS.index(filter_name),
+                                    kernel_idx)
     if rc != 0:
         raise ValueError(f"oracle filter {filter_name}/{kernel_idx} unsupported (rc={rc})")
-    return out
+    return (out, und.astype(bool)) if with_undefined else out
+
+
+def defined_mask(width, height, refs_undefined=None):
+    """Bool mask over a frame's cost table: entries the reference defines.  Geometric part:
+    layout.available_mask (the engine's UNAVAILABLE set is its complement); with a filtered
+    reference frame, also the CUs none of whose reference samples is undefined."""
+    from mipgpu import layout
+    m = layout.available_mask(width, height)
+    if refs_undefined is None or not refs_undefined.any():
+        return m
+    cu = np.zeros(layout.num_ctus(width, height) * layout.CUS_PER_CTU, np.uint8)
+    lib().mipo_ref_undefined_cus(np.ascontiguousarray(refs_undefined, np.uint8), width, height, cu)
+    return m & ~layout.expand_cu_mask(cu.astype(bool), layout.num_ctus(width, height))
 
 
 def synth(width, height, seed, kind=0):

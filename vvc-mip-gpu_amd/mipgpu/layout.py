@@ -99,19 +99,42 @@ def ctu_entries():
     return dict(shape=shape, cu=cu, mode=mode, x=x, y=y, w=w, h=h)
 
 
-def available_mask(width: int, height: int) -> np.ndarray:
-    """Boolean mask over a frame's cost table: True where the CU lies inside the frame.
+def cu_defined(width: int, height: int, x, y, w, h):
+    """Does the reference define the cost of the CU at frame position (x, y)?
 
-    The reference leaves these entries undefined (stale LDS, intra.cl:96-98, 717);
-    this engine writes UNAVAILABLE there.
+    The reference reads samples by linear index y' * W + x' (intra.cl:100, 106, 236, 242,
+    718): a CU right of the frame reads the next row's samples, deterministically, as long
+    as every index stays below W * H; its largest index is its bottom-right original sample.
+    CUs with y + h > H are skipped by initBoundaries (stale LDS, intra.cl:96-98, 232-234).
     """
+    return (y + h < height) | ((y + h == height) & (x + w <= width))
+
+
+def available_mask(width: int, height: int) -> np.ndarray:
+    """Boolean mask over a frame's cost table: True where the reference defines the cost
+    (cu_defined); this engine writes UNAVAILABLE everywhere else."""
     e = ctu_entries()
     cols, rows = ctu_grid(width, height)
     ctu = np.arange(cols * rows)
     cx = (128 * (ctu % cols))[:, None]
     cy = (128 * (ctu // cols))[:, None]
-    ok = (cx + e["x"][None, :] + e["w"][None, :] <= width) & (cy + e["y"][None, :] + e["h"][None, :] <= height)
+    ok = cu_defined(width, height, cx + e["x"][None, :].astype(np.int64), cy + e["y"][None, :].astype(np.int64),
+                    e["w"][None, :], e["h"][None, :])
     return ok.reshape(-1)
+
+
+@lru_cache(maxsize=None)
+def _entry_cu():
+    """CU index (CU order inside the CTU) of each of the 97840 cost entries."""
+    prefix = np.cumsum([0] + [s.ncu for s in SHAPES])
+    e = ctu_entries()
+    return (prefix[e["shape"]] + e["cu"]).astype(np.int32)
+
+
+def expand_cu_mask(cu_mask: np.ndarray, nctus: int) -> np.ndarray:
+    """Per-CU bool mask (nctus * 5380, CU order) -> per-cost-entry mask (nctus * 97840)."""
+    m = np.asarray(cu_mask, bool).reshape(nctus, CUS_PER_CTU)
+    return m[:, _entry_cu()].reshape(-1)
 
 
 def cu_count(nctus: int) -> int:
