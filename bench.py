@@ -10,6 +10,10 @@ and the max-over-ranks of the timing) -> weak scaling.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step B]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Without a launcher (WORLD_SIZE unset), `--gpus N` > 1 starts the N ranks itself (one child
+process per GPU, before anything touches the GPU) and exits with their status; under a
+launcher, `--gpus` must equal WORLD_SIZE.
+
 Rank 0 prints one JSON line (contract in the task statement), plus:
   roofline      HBM roofline of the search kernel (algorithmic bytes = frame read + int32
                 cost write, per launch) with the launch time from HIP events on the stream
@@ -61,6 +65,51 @@ E2E_CALLS = 8  # host-buffer calls queued per end-to-end measurement
 
 def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`--gpus n` without a launcher: start n ranks of this script (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1), wait for them and
+    return the worst exit status.  Nothing in this process touches the GPU.  A rank that
+    fails ends the others (they would wait at the barrier)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def gather_ranks(values, world, device=None):
+    """All ranks' `values` (list of floats) -> [world][len(values)] (nccl or gloo)."""
+    if world <= 1:
+        return [list(values)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [[float(v) for v in o.cpu()] for o in out]
 
 
 def dist_max(value, world, device=None):
@@ -199,6 +248,46 @@ def reference_gpu(width, height, frames, seed):
         return {"error": str(exc)[:200]}
 
 
+def ranks_section(per_rank, frames_per_step, steps, backend):
+    """Rank count actually running (dist.get_world_size()) and each rank's own rate (its own
+    search launches' device time: the wall time between the barriers is the slowest rank's
+    for every rank)."""
+    world = len(per_rank)
+    if world > 1:
+        import torch.distributed as dist
+        world = dist.get_world_size()
+    return {"world_size": world, "backend": backend,
+            "per_rank_frames_per_s": [round(frames_per_step / (r[1] * 1e-3), 2) for r in per_rank],
+            "per_rank_kernel_ms": [round(r[1], 4) for r in per_rank]}
+
+
+def plumbing_check(args):
+    """--plumbing-check: the multi-rank path of main() on CPU (gloo), a sleep per step."""
+    import torch.distributed as dist
+    rank, _, world = dist_env()
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.01 * (1 + rank))  # rank r is the (r+1)-times slower one
+    own = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per_rank = gather_ranks([elapsed, 1e3 * own / args.steps], world)
+    max_elapsed = max(r[0] for r in per_rank)
+    value, ms_per_step = aggregate(args.frames_per_step, args.steps, world, max_elapsed)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+                          "data": "plumbing check (no GPU, sleep per step)",
+                          "ranks": ranks_section(per_rank, args.frames_per_step, args.steps,
+                                                 "gloo" if world > 1 else None)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,7 +308,19 @@ def main():
                     help="alternative references: run this reference filter (e.g. filterFrame_2d_int_quarterCtu) "
                          "inside every step (BASELINE configs[2]/[4]); default: original references")
     ap.add_argument("--kernel-idx", type=int, default=0, help="KernelIdx of --refs-filter")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="CPU only (gloo): run the rank launch, timing reduction and JSON line with a "
+                         "sleep in place of the search (tests/test_bench_dist.py)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks" % (args.gpus, os.environ["WORLD_SIZE"]),
+              file=sys.stderr)
+        sys.exit(2)
+    if args.plumbing_check:
+        return plumbing_check(args)
 
     import numpy as np
     import torch
@@ -262,8 +363,9 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one search launch per step, same stream
 
-    max_elapsed = dist_max(elapsed, world, dev)
-    max_kernel_ms = dist_max(kernel_ms, world, dev)
+    per_rank = gather_ranks([elapsed, kernel_ms], world, dev)
+    max_elapsed = max(r[0] for r in per_rank)
+    max_kernel_ms = max(r[1] for r in per_rank)
     value, ms_per_step = aggregate(B, args.steps, world, max_elapsed)
 
     cfg = {(1920, 1080, None): 1, (1920, 1080, "filterFrame_2d_float_5x5_quarterCtu"): 2, (3840, 2160, None): 3,
@@ -292,6 +394,7 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes},
             # The bound that applies: VALU issue (see the module docstring).
             "valu": valu_section(pmc, max_kernel_ms, ops),
+            "ranks": ranks_section(per_rank, B, args.steps, "nccl" if world > 1 else None),
         }
         if world == 1 and not args.no_filter:
             res["filter"] = filter_section(MipEngine, frames, W, H, B, stream, dev, 5, pmc)

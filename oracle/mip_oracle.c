@@ -234,7 +234,7 @@ static void cu_distortion(const uint16_t *orig, int width, int x, int y, int w, 
  * (y + h - 1) * W + x + w - 1 (its reference row / column indexes are smaller).  CUs with
  * y + h > H are skipped by initBoundaries (intra.cl:96-98, 232-234): stale LDS. */
 int mipo_cu_defined(int width, int height, int x, int y, int w, int h) {
-  return y + h < height || (y + h == height && x + w <= width);
+  return y + h <= height && (long long)(y + h - 1) * width + x + w - 1 < (long long)width * height;
 }
 
 static void search_ctu(const uint16_t *orig, const uint16_t *refs, int width, int height,
@@ -336,7 +336,9 @@ static float ref_fdiv(float v, int s) {
  * tile_sep5 fill the tile's LDS the way the reference does and compute its 128 x rows
  * outputs, each with a POISON flag = "depends on memory outside this frame" (a read at a
  * linear index >= W * H: the next frame slot or the buffer's padding, never written for this
- * frame).  filter_run then writes them like the reference (see there).
+ * frame).  A poisoned cell reads 0 (as the HIP kernel does), so poisoned outputs still get
+ * a value -- one the reference does not define.  filter_run then writes them like the
+ * reference (see there).
  *
  * LDS cell: value, or -1 for a cell the reference marks invalid, and the poison flag. */
 typedef struct {
@@ -406,11 +408,11 @@ static void tile_2d(const uint16_t *in, int W, int H, int qx, int qy, const uint
           const cell_t e = t[(r + dy + R) * P + c + dx + R];
           const int k = taps[(dy + R) * ksz + dx + R];
           poison |= e.p;
-          if (e.p || e.v < 0) continue;
+          if (e.v < 0) continue;
           sum += k * e.v;
           scale += k;
         }
-      ov[r * 128 + c] = poison ? 0 : (int16_t)round_div(sum, scale, is_float);
+      ov[r * 128 + c] = (int16_t)round_div(sum, scale, is_float);
       op[r * 128 + c] = (uint8_t)poison;
     }
 }
@@ -468,7 +470,7 @@ static void tile_sep3(const uint16_t *in, int W, int H, int X, int Y, const uint
       int res;
       if (is_float) res = (int)roundf(ref_fdiv((float)v, sc));
       else res = ((int)v + sc / 2) / sc;
-      ov[r * 128 + c] = poison ? 0 : (int16_t)res;
+      ov[r * 128 + c] = (int16_t)res;
       op[r * 128 + c] = (uint8_t)poison;
     }
 }
@@ -593,7 +595,7 @@ static void tile_sep5(const uint16_t *in, int W, int H, int X, int Y, const uint
       int res;
       if (is_float) res = (int)roundf(ref_fdiv((float)v, sc));
       else res = ((int)v + sc / 2) / sc;
-      ov[r * 128 + c] = poison ? 0 : (int16_t)res;
+      ov[r * 128 + c] = (int16_t)res;
       op[r * 128 + c] = (uint8_t)poison;
     }
 }

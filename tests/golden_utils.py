@@ -33,10 +33,27 @@ def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def masked(table, width, height):
-    t = np.array(table, dtype="<i4", copy=True).reshape(-1)
-    t[~layout.available_mask(width, height)] = layout.UNAVAILABLE
+def refs_and_mask(fx, frames, f):
+    """(filtered reference frame or None, its undefined-sample mask or None, defined-entry
+    mask of the cost table) of frame f of a fixture, from the C oracle (the fixture's
+    fill_check shows the oracle's undefined set covers every entry the reference left
+    undefined in the fill experiment, see tools/ref_golden.py)."""
+    import oracle_lib as O
+    c = fx["config"]
+    refs, und = (None, None)
+    if c["filter"]:
+        refs, und = O.filter_frame(frames[f], c["filter"], c["kernel_idx"], with_undefined=True)
+    return refs, und, O.defined_mask(c["width"], c["height"], und)
+
+
+def masked(table, mask, fill=layout.UNAVAILABLE):
+    t = np.array(table, copy=True).reshape(-1)
+    t[~np.asarray(mask).reshape(-1)] = fill
     return t
+
+
+def filtered_sha(frame, undefined):
+    return sha(masked(np.asarray(frame, "<u2"), ~undefined, 0xFFFF))
 
 
 def ctu_row(fx, frame, ctu):

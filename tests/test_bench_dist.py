@@ -52,3 +52,32 @@ def test_aggregate_is_whole_job_throughput():
     v, ms = bench.aggregate(frames_per_step=8, steps=10, world=4, max_elapsed_s=2.0)
     assert v == 8 * 10 * 4 / 2.0 and ms == 200.0
     assert bench.algorithmic_bytes_per_frame(1920, 1080) == 1920 * 1080 * 2 + 135 * 97840 * 4
+
+
+def test_gpus_flag_without_launcher_starts_ranks():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (gloo plumbing check on
+    CPU): world size 2 in the line, value = all ranks' frames / the slowest rank's time."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--plumbing-check", "--steps", "5",
+                        "--frames-per-step", "4"], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["ranks"]["world_size"] == 2 and line["ranks"]["backend"] == "gloo"
+    per = line["ranks"]["per_rank_frames_per_s"]
+    assert len(per) == 2 and per[0] > per[1]          # rank 1 sleeps twice as long
+    # whole-job rate: 2 ranks x 5 steps x 4 frames over the slowest rank's time (between the
+    # barriers), so at most twice the slow rank's own rate
+    assert abs(line["value"] - 2 * 5 * 4 / (5 * line["ms_per_step"] * 1e-3)) / line["value"] < 1e-3
+    assert line["value"] <= 2 * per[1] * 1.001
+
+
+def test_gpus_flag_must_match_launcher():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "4", "--plumbing-check"], capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

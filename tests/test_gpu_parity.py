@@ -23,28 +23,39 @@ def _engine(c, **kw):
                      max_batch=c["frames"], **kw)
 
 
-@pytest.mark.parametrize("name", [n for n in G.names() if n.startswith("small_")])
+SMALL = [n for n in G.names() if n.startswith(("small_", "w416", "w832", "w1280"))]
+
+
+@pytest.mark.parametrize("name", SMALL)
 def test_small_configs_vs_oracle_and_reference(gpu_available, name):
+    """Small sizes and the reference's own resolutions whose width is not a multiple of 128
+    (416x240, 832x480, 1280x720: CUs right of the frame read the next row, the filters'
+    racing stores): bit-exact vs the oracle everywhere, and the defined entries hash to the
+    reference's."""
     fx = G.load(name)
     c = fx["config"]
     frames = G.inputs(fx)
     with _engine(c, want_sad_satd=True) as eng:
         out = eng.search(frames, sad_satd=True)
+        filt = eng.filter_frames(frames, c["filter"], c["kernel_idx"]) if c["filter"] else None
     for f, fr in enumerate(fx["frames"]):
-        refs = O.filter_frame(frames[f], c["filter"], c["kernel_idx"]) if c["filter"] else None
+        refs, und, mask = G.refs_and_mask(fx, frames, f)
         oc, osad, osatd = O.search(frames[f], refs, want_sad_satd=True)
         assert np.array_equal(out["cost"][f], oc)
         assert np.array_equal(out["sad"][f], osad)
         assert np.array_equal(out["satd"][f], osatd)
-        assert G.sha(G.masked(out["cost"][f], c["width"], c["height"])) == fr["cost_sha256"]
+        assert G.sha(G.masked(out["cost"][f], mask)) == fr["cost_sha256"]
         if "sad_sha256" in fr:
-            assert G.sha(G.masked(out["sad"][f], c["width"], c["height"])) == fr["sad_sha256"]
-            assert G.sha(G.masked(out["satd"][f], c["width"], c["height"])) == fr["satd_sha256"]
+            assert G.sha(G.masked(out["sad"][f], mask)) == fr["sad_sha256"]
+            assert G.sha(G.masked(out["satd"][f], mask)) == fr["satd_sha256"]
+        if filt is not None:
+            assert np.array_equal(filt[f], refs)
+            assert G.filtered_sha(filt[f], und) == fr["filtered_sha256"]
 
 
-@pytest.mark.parametrize("name", [n for n in G.names() if not n.startswith("small_")])
+@pytest.mark.parametrize("name", [n for n in G.names() if n not in SMALL])
 def test_full_size_configs_vs_reference(gpu_available, name):
-    """1080p / 4K: the whole masked cost table hashes to the reference's."""
+    """1080p / 4K: the whole cost table, defined entries, hashes to the reference's."""
     fx = G.load(name)
     c = fx["config"]
     frames = G.inputs(fx)
@@ -53,13 +64,15 @@ def test_full_size_configs_vs_reference(gpu_available, name):
         if c["filter"]:
             filt = eng.filter_frames(frames, c["filter"], c["kernel_idx"])
     for f, fr in enumerate(fx["frames"]):
-        assert G.sha(G.masked(out["cost"][f], c["width"], c["height"])) == fr["cost_sha256"]
+        refs, und, mask = G.refs_and_mask(fx, frames, f)
+        # the engine's UNAVAILABLE entries are exactly the geometrically undefined CUs
+        assert np.array_equal(out["cost"][f] == layout.UNAVAILABLE, ~layout.available_mask(c["width"], c["height"]))
+        assert G.sha(G.masked(out["cost"][f], mask)) == fr["cost_sha256"]
         for ctu in map(int, fr["ctu_rows"]):
-            row = out["cost"][f][ctu * 97840:(ctu + 1) * 97840]
-            m = layout.available_mask(c["width"], c["height"])[ctu * 97840:(ctu + 1) * 97840]
-            assert np.array_equal(np.where(m, row, layout.UNAVAILABLE), G.ctu_row(fx, f, ctu))
+            sl = slice(ctu * 97840, (ctu + 1) * 97840)
+            assert np.array_equal(G.masked(out["cost"][f][sl], mask[sl]), G.ctu_row(fx, f, ctu))
         if c["filter"]:
-            assert G.sha(filt[f]) == fr["filtered_sha256"]
+            assert G.filtered_sha(filt[f], und) == fr["filtered_sha256"]
 
 
 @pytest.mark.parametrize("w,h", [(392, 136), (648, 232), (300, 68), (292, 36)])

@@ -109,14 +109,19 @@ __device__ __forceinline__ bool sep_fetch(int qx, int qy, int ty, int tc, int W,
   return g > 0 && g < WH && qx + tc > 0 && qx + tc < W - 1;
 }
 
-// Tile cell inside the 128x32 tile: 2-D -- valid iff inside the frame, else -1; separable
-// 3 taps -- always fetched, samples outside the frame read 0 (intra.cl:3330, unguarded);
-// separable 5 taps -- fetched for frame rows (outside columns read 0), else -1.
+// Tile cell inside the 128x32 tile, read like the reference: by linear index y * W + x, so
+// columns right of the frame are the next row's first samples (intra.cl:2905, 3098, 3331,
+// 3597).  Rows below the frame: 2-D and separable 5 taps -1 (invalid), separable 3 taps read
+// them unguarded (intra.cl:3330-3332, past the frame's end).  Reads past the frame's end give
+// outputs the reference leaves undefined (they depend on the next frame slot); they read 0
+// here.
 template <int RAD, bool SEP>
 __device__ __forceinline__ short inner_value(const uint16_t *in, int x, int y, int W, int H) {
-  if (y < H && x < W) return (short)in[(size_t)y * W + x];
-  if (!SEP) return -1;
-  return (RAD == 1 || y < H) ? 0 : -1;
+  if (y < H) {
+    const int li = y * W + x;
+    return li < W * H ? (short)in[li] : 0;
+  }
+  return (SEP && RAD == 1) ? 0 : -1;
 }
 
 // Stage the tile (+halo) in LDS: interior rows with 16-byte loads when the rows are
@@ -172,17 +177,17 @@ __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, i
     hidx[p] = (ty + RAD) * kTWP + kCO + tc;
   }
   if ((W & 7) == 0) {
-    // W % 8 == 0: a chunk of 8 columns lies entirely inside or entirely outside the frame,
-    // and an outside chunk reads nothing (inner_value's fill for x >= W or y >= H)
+    // W % 8 == 0: a chunk of 8 columns lies entirely inside or entirely outside the frame's
+    // linear extent; rows below the frame and indexes past its end read inner_value's fill
     uint4 v[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) {
       const int i = p * kThreads + t, r = i >> 4, k = i & 15;
       const int y = qy + r, x = qx + 8 * k;
-      if (y < H && x + 8 <= W) {
-        v[p] = *reinterpret_cast<const uint4 *>(in + (size_t)y * W + x);
+      if (y < H && y * W + x + 8 <= W * H) {
+        v[p] = *reinterpret_cast<const uint4 *>(in + y * W + x);
       } else {
-        const short fv = !SEP ? -1 : ((RAD == 1 || y < H) ? 0 : -1);
+        const short fv = (y < H || (SEP && RAD == 1)) ? 0 : -1;
         invalid |= fv < 0;
         const uint32_t f2 = (uint32_t)(uint16_t)fv * 0x10001u;
         v[p] = make_uint4(f2, f2, f2, f2);

@@ -59,6 +59,7 @@ struct SearchArgs {
                           // [list_begin[l], list_begin[l+1])
   const uint32_t *fill;   // unavailable cost entries of (v, q) (uint4 units inside the CTU's cost
   const int *fill_begin;  // block): [fill_begin[4v+q], fill_begin[4v+q+1])
+  const uint8_t *ctu_var; // [nctus] CTU variant (mipgpu.cpp ctu_variants): which CUs are defined
   const uint4 *tables;    // kTableBytes: MIP matrices for the MFMA, see below
   int width, height;
   int ctu_cols, nctus;
@@ -72,9 +73,9 @@ struct SearchArgs {
                           // task of the workgroup's list; else null
 };
 constexpr int kClockSlots = 128;
-// CTU variants: bit 0 = the frame ends inside the CTU horizontally, bit 1 = vertically
-// (mipgpu.cpp build_work); their lists omit the CUs that are not completely inside the frame.
-constexpr int kCtuVariants = 4;
+// CTU variants (mipgpu.cpp ctu_variants): CTUs with the same set of defined CUs share work /
+// fill lists; the lists omit the CUs whose cost the reference leaves undefined.
+constexpr int kMaxCtuVariants = 255;
 
 // MIP matrices, restated for an exact f16 MFMA (mip_search.hip, phase A).  The reference
 // computes pred_j = clamp(((32 - 32*sum_k p_k + sum_k p_k*w_jk) >> 6) + b0, 0, 1023) with

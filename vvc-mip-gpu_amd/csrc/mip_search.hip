@@ -848,18 +848,27 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
 }
 
 // Stage the quadrant window (rows -1..63, columns -4..63) of one frame into LDS, each
-// sample plus its residual bias (kBiasD).  Samples outside the frame read as 0 (+ bias);
-// they only feed CUs whose results are discarded or padding branches that never select them.
+// sample plus its residual bias (kBiasD).  Samples are addressed like the reference does,
+// by linear index fy * W + fx (intra.cl:100, 106, 236, 242, 718): columns right of the frame
+// read the next row's first samples, so CUs right of the frame get the reference's
+// (deterministic) costs.  Indexes past the frame's end and the columns left of a frame's
+// first column read as 0 (+ bias): they only feed CUs whose costs the reference leaves
+// undefined (no task) or padding branches that never select them.
 constexpr int kTileChunks = kPitch / 4;            // 17 chunks of 4 samples per row
 constexpr int kTileLoads = 65 * kTileChunks;       // 1105 8-byte chunks per quadrant window
 
+// 8-byte chunk at linear index fy * width + fx (fx % 4 == 0, width % 4 == 0: a chunk lies
+// entirely inside or entirely outside [0, width * height)).
+__device__ __forceinline__ uint2 frame_chunk(const uint16_t *frame, int width, int height, int fx, int fy) {
+  const int li = fy * width + fx;
+  uint2 v = make_uint2(0, 0);
+  if (fy >= 0 && fx >= 0 && li < width * height) v = *reinterpret_cast<const uint2 *>(frame + li);
+  return v;
+}
+
 __device__ __forceinline__ uint2 tile_load(const uint16_t *frame, int width, int height, int x0, int y0, int i) {
   const int row = i / kTileChunks, ch = i - row * kTileChunks;
-  const int fy = y0 - 1 + row, fx = x0 - kColOff + 4 * ch;
-  uint2 v = make_uint2(0, 0);
-  if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
-    v = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
-  return v;
+  return frame_chunk(frame, width, height, x0 - kColOff + 4 * ch, y0 - 1 + row);
 }
 
 __device__ __forceinline__ void tile_store(uint16_t *dst, int i, uint2 v) {
@@ -901,7 +910,8 @@ struct ItemPos {
   }
 };
 
-// Stage the reference lattice (ALT): rows 4i-1 (columns -4..63), columns 4i-1 (rows -1..63).
+// Stage the reference lattice (ALT): rows 4i-1 (columns -4..63), columns 4i-1 (rows -1..63),
+// by linear index like the window (frame_chunk).
 __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
                                               int x0, int y0) {
   // all loads first, then all LDS stores (as stage_tile)
@@ -912,16 +922,13 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
 #pragma unroll
   for (int k = 0; k < NRL; k++) {
     const int i = min((int)threadIdx.x + NT * k, NR - 1), row = i / kChunks, ch = i - row * kChunks;
-    const int fy = y0 + 4 * row - 1, fx = x0 - kColOff + 4 * ch;
-    rv[k] = make_uint2(0, 0);
-    if (fy >= 0 && fy < height && fx >= 0 && fx + 4 <= width)
-      rv[k] = *reinterpret_cast<const uint2 *>(frame + (size_t)fy * width + fx);
+    rv[k] = frame_chunk(frame, width, height, x0 - kColOff + 4 * ch, y0 + 4 * row - 1);
   }
 #pragma unroll
   for (int k = 0; k < NCL; k++) {
     const int i = min((int)threadIdx.x + NT * k, NC - 1), col = i / 65, yy = i - col * 65;
-    const int fy = y0 + yy - 1, fx = x0 + 4 * col - 1;
-    cv[k] = (fy >= 0 && fy < height && fx >= 0 && fx < width) ? frame[(size_t)fy * width + fx] : 0;
+    const int fy = y0 + yy - 1, fx = x0 + 4 * col - 1, li = fy * width + fx;  // linear, as frame_chunk
+    cv[k] = (fy >= 0 && fx >= 0 && li < width * height) ? frame[li] : 0;
   }
 #pragma unroll
   for (int k = 0; k < NRL; k++) {
@@ -991,15 +998,15 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     const ItemPos ip(a, item);
     const int ctu = ip.ctu, frame = ip.frame, slice = ip.slice, quad = ip.quad, fx0 = ip.fx0, fy0 = ip.fy0;
     const size_t fofs = (size_t)frame * a.width * a.height;
-    const int var = (ip.ctu_x + 128 > a.width ? 1 : 0) | (ip.ctu_y + 128 > a.height ? 2 : 0);
+    const int var = a.ctu_var[ctu];  // work / fill lists of the CTU's variant (mipgpu.cpp ctu_variants)
     const int vq = var * 4 + quad, list = vq * a.slices + slice;
     const int tbase = a.list_begin[list], ntasks = a.list_begin[list + 1] - tbase;
     uint16_t *org = org_buf + (PF ? par * kTileElems : 0);
     uint16_t *ref = ALT ? lattice : org;
 
-    // CUs not completely inside the frame (edge CTUs): MIP_COST_UNAVAILABLE, no search
+    // CUs whose cost the reference leaves undefined (edge CTUs): MIP_COST_UNAVAILABLE, no search
     // (decisions only: their entries keep the launch's all-ones = unavailable)
-    if (var && !DEC) {
+    if (!DEC) {
       const size_t cbase = ((size_t)frame * a.nctus + ctu) * (MIP_COSTS_PER_CTU / 4);
       const int f0 = a.fill_begin[vq], nf = a.fill_begin[vq + 1] - f0;
       const uint4 un = make_uint4(kUnavailable, kUnavailable, kUnavailable, kUnavailable);

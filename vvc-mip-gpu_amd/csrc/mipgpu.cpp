@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -101,11 +102,15 @@ std::vector<uint8_t> build_tables() {
 // lists (one per workgroup); each list stays in decreasing cost order, and the waves of a
 // workgroup take its tasks dynamically.  Costs are VALU-instruction estimates per lane.
 // MIPGPU_SHAPE_FILTER="i,j,..." (profiling knob) restricts the search to those shapes.
-// Edge CTUs: a CTU in the last column / row of a frame whose width / height is not a
-// multiple of 128 holds CUs that are not completely inside the frame (the reference leaves
-// their costs undefined, here they are MIP_COST_UNAVAILABLE).  Such CUs get no task: each of
-// the 4 CTU variants (bit 0: partial width, bit 1: partial height) has its own lists, and a
-// fill list of the unavailable cost entries (16-byte units inside the CTU's cost block).
+// Edge CTUs: the reference reads samples by linear index (intra.cl:100, 236, 718), so CUs
+// right of the frame read the next row (defined costs, searched here too) and only two
+// kinds of CU are undefined (MIP_COST_UNAVAILABLE here): CUs below the frame (y + h > H:
+// stale LDS, intra.cl:96-98) and CUs whose bottom-right sample's linear index
+// (y + h - 1) * W + x + w - 1 is past the frame end (in practice: touching the bottom row
+// and reaching past the right edge).  Such CUs get no task.  CTUs with the same set of
+// defined CUs share a *variant* (ctu_variants: usually the interior, the last CTU row and
+// the last CTU); each variant has its own lists and a fill list of the unavailable cost
+// entries (16-byte units inside the CTU's cost block).
 struct WorkLists {
   std::vector<mipgpu::WaveTask> tasks;
   std::vector<mipgpu::Job> jobs;
@@ -140,6 +145,43 @@ bool no_pairs() {
 }
 
 // Estimated VALU instructions per lane for one mode pair of a task of `ncu` CUs.
+// Is the cost of the CU at frame position (x, y) defined (mipgpu.layout.cu_defined,
+// oracle mipo_cu_defined)?
+bool cu_defined(int width, int height, int x, int y, int w, int h) {
+  return y + h <= height && (long long)(y + h - 1) * width + x + w - 1 < (long long)width * height;
+}
+
+// CTU -> variant (index of the CTU's set of defined CUs), and each variant's first CTU.
+struct CtuVariants {
+  std::vector<uint8_t> of_ctu;
+  std::vector<int> rep;
+};
+
+CtuVariants ctu_variants(int width, int height) {
+  CtuVariants v;
+  const int cols = (width + 127) / 128, n = cols * ((height + 127) / 128);
+  std::vector<std::vector<bool>> seen;
+  for (int c = 0; c < n; c++) {
+    const int cx = 128 * (c % cols), cy = 128 * (c / cols);
+    std::vector<bool> pat;
+    pat.reserve(MIP_CUS_PER_CTU);
+    for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+      const mip_shape_desc &sd = kShapes[s];
+      for (int cu = 0; cu < sd.ncu; cu++)
+        pat.push_back(cu_defined(width, height, cx + axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols),
+                                 cy + axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols), sd.w, sd.h));
+    }
+    size_t k = 0;
+    while (k < seen.size() && seen[k] != pat) k++;
+    if (k == seen.size()) {
+      seen.push_back(pat);
+      v.rep.push_back(c);
+    }
+    v.of_ctu.push_back((uint8_t)k);
+  }
+  return v;
+}
+
 double pair_cost(int cls, int ncu) {
   const int w = mipgpu::kClassW[cls], h = mipgpu::kClassH[cls];
   const int sid = mipgpu::class_size_id(w, h), v = mipgpu::kClassV[cls];
@@ -149,13 +191,12 @@ double pair_cost(int cls, int ncu) {
   return blocks * 200.0 + mfma * 12.0 + 40.0;
 }
 
-WorkLists build_work(int slices, int waves, int width, int height) {
+WorkLists build_work(int slices, int waves, int width, int height, const CtuVariants &cv) {
   WorkLists wl;
-  for (int vq = 0; vq < 4 * mipgpu::kCtuVariants; vq++) {
+  const int cols = (width + 127) / 128;
+  for (int vq = 0; vq < 4 * (int)cv.rep.size(); vq++) {
     const int var = vq / 4, q = vq % 4;
-    // samples of the CTU inside the frame (variant 0: the whole CTU)
-    const int avw = (var & 1) && width % 128 ? width % 128 : 128;
-    const int avh = (var & 2) && height % 128 ? height % 128 : 128;
+    const int cx = 128 * (cv.rep[var] % cols), cy = 128 * (cv.rep[var] / cols);  // the variant's first CTU
     wl.fill_begin.push_back((int)wl.fill.size());
     struct Piece { mipgpu::WaveTask t; double cost; };
     std::vector<Piece> pieces;
@@ -168,7 +209,7 @@ WorkLists build_work(int slices, int waves, int width, int height) {
       for (int cu = 0; cu < sd.ncu; cu++) {
         const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
         if (x / 64 != (q & 1) || y / 64 != (q >> 1)) continue;
-        if (x + sd.w > avw || y + sd.h > avh) {
+        if (!cu_defined(width, height, cx + x, cy + y, sd.w, sd.h)) {
           const uint32_t off = sd.cost_offset + cu * 2 * sd.modes;  // multiple of 4 entries
           for (uint32_t u = 0; u < (uint32_t)(2 * sd.modes) / 4; u++) wl.fill.push_back(off / 4 + u);
           continue;
@@ -292,6 +333,7 @@ struct mip_engine {
   };
   std::vector<Work> work;
   uint8_t *d_tables = nullptr;
+  uint8_t *d_ctu_var = nullptr;  // [nctus] CTU variant (ctu_variants)
   int resident[2] = {0, 0};  // persistent search grid (workgroups resident on this device), [alt]
   // Engine-owned reference scratch d_refs, written by the engine filter when a device-API
   // search has no caller references: every such search records refs_done on its stream, and
@@ -386,7 +428,8 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   if (e->stream3) (void)hipStreamSynchronize(e->stream3);
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
-                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables})
+                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables,
+                  (void *)e->d_ctu_var})
     if (p) (void)hipFree(p);
   if (e->d_queue) (void)hipFree(e->d_queue);
   for (hipEvent_t ev : e->queue_done)
@@ -413,6 +456,10 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   *out = nullptr;
   if (width <= 0 || height <= 0 || width % 4 || height % 4)
     return fail("frame size %dx%d must be positive multiples of 4", width, height);
+  // 32-bit linear sample indexes in the kernels (the window reaches 128 columns and 64 rows
+  // past the frame)
+  if ((long long)(width + 128) * (height + 128) >= (1LL << 31))
+    return fail("frame size %dx%d too large (linear sample index beyond 2^31)", width, height);
   mip_opts o;
   mip_opts_default(&o);
   if (opts) o = *opts;
@@ -474,11 +521,16 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0)) < 1)
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
+  const CtuVariants cv = ctu_variants(width, height);
+  if (cv.rep.size() > (size_t)mipgpu::kMaxCtuVariants) return cleanup(fail("too many CTU variants (%zu)", cv.rep.size()));
+  ALLOC(e->d_ctu_var, cv.of_ctu.size());
+  if (hipMemcpy(e->d_ctu_var, cv.of_ctu.data(), cv.of_ctu.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(fail("uploading CTU variants failed"));
   std::vector<int> slice_set;
   if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
   else slice_set = {1, 2, 4};
   for (int sl : slice_set) {
-    const WorkLists wl = build_work(sl, mipgpu::search_waves_per_group(), width, height);
+    const WorkLists wl = build_work(sl, mipgpu::search_waves_per_group(), width, height, cv);
     mip_engine::Work w;
     w.slices = sl;
     e->work.push_back(w);
@@ -571,6 +623,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.fill = work.d_fill;
   a.fill_begin = work.d_fill_begin;
   a.tables = reinterpret_cast<const uint4 *>(e->d_tables);
+  a.ctu_var = e->d_ctu_var;
   a.width = e->width;
   a.height = e->height;
   a.ctu_cols = e->ctu_cols;
@@ -588,10 +641,10 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     HIP_TRY(hipMalloc((void **)&a.wave_clock, n * 8));
     HIP_TRY(hipMemsetAsync(a.wave_clock, 0, n * 8, s));
     clocks.resize(n);
-    static bool dumped = false;
-    if (!dumped) {
-      dumped = true;
-      const WorkLists wl = build_work(work.slices, mipgpu::search_waves_per_group(), e->width, e->height);
+    static std::atomic<bool> dumped{false};
+    if (!dumped.exchange(true)) {
+      const WorkLists wl = build_work(work.slices, mipgpu::search_waves_per_group(), e->width, e->height,
+                                      ctu_variants(e->width, e->height));
       if (FILE *f = fopen((std::string(timing) + ".tasks").c_str(), "w")) {
         fprintf(f, "{\"slices\": %d, \"list_begin\": [", work.slices);
         for (size_t i = 0; i < wl.list_begin.size(); i++) fprintf(f, "%s%d", i ? ", " : "", wl.list_begin[i]);

@@ -107,7 +107,8 @@ def cu_defined(width: int, height: int, x, y, w, h):
     as every index stays below W * H; its largest index is its bottom-right original sample.
     CUs with y + h > H are skipped by initBoundaries (stale LDS, intra.cl:96-98, 232-234).
     """
-    return (y + h < height) | ((y + h == height) & (x + w <= width))
+    y = np.asarray(y, np.int64)
+    return (y + h <= height) & ((y + h - 1) * width + x + w - 1 < width * height)
 
 
 def available_mask(width: int, height: int) -> np.ndarray:
