@@ -393,16 +393,20 @@ def test_async_host_calls_and_device_filter_scratch(gpu_available):
 
 
 @pytest.mark.parametrize("w,h,filt,k", [(264, 200, None, 0), (136, 72, None, 0),
-                                        (392, 264, "filterFrame_2d_float_5x5_quarterCtu", 2)])
+                                        (392, 264, "filterFrame_2d_float_5x5_quarterCtu", 2),
+                                        (416, 240, "filterFrame_1d_int_5x5", 2)])
 def test_device_decisions_only_fused_argmin(gpu_available, w, h, filt, k):
     """mip_search_device without a cost table (costs=False): the search keeps each CU's
     argmin (cost << 5 | mode, atomicMin per task -- tasks that cut a CU's mode pairs meet in
     one entry) and unpacks it; must equal the argmin of the oracle's table (ties to the lower
     mode, unavailable CUs 0xff / MIP_COST_UNAVAILABLE), for 1..3-frame batches (different
-    task cuts per slice count)."""
+    task cuts per slice count).  416x240 with a separable filter: reference samples above 10
+    bits in the last columns (the exact per-CU kernel's CUs write their argmin directly)."""
     import torch
     n = 3
     frames = synth_frames(w, h, n, 0xD0 + w, 1)
+    if w == 416:
+        assert max(O.filter_frame(frames[f], filt, k).max() for f in range(n)) > 1023
     nct = layout.num_ctus(w, h)
     want = []
     for f in range(n):

@@ -30,6 +30,7 @@
 #include <fstream>
 #include <iostream>
 #include <sstream>
+#include <memory>
 #include <string>
 #include <condition_variable>
 #include <mutex>
@@ -325,24 +326,28 @@ struct ShapeInfo {
   std::vector<int> x, y;
 };
 
-// Rows formatted by CTU chunks on `threads` threads, written in chunk order; at most
-// `threads` chunk buffers exist at a time (an 8K frame's cost log is ~11 GB of text).
+// Rows formatted by CTU chunks on up to kMaxLiveChunks threads, written in chunk order.  Host
+// memory is bounded independently of the thread count: at most kMaxLiveChunks chunk buffers
+// exist, each allocated once without zero-filling (only the pages a chunk's rows touch are
+// committed -- ~55 bytes per row against the chunk_bytes bound), and reused round after
+// round (an 8K frame's cost log is ~11 GB of text).
 // format(c, p) writes chunk c's rows at p and returns the end; chunk_bytes bounds them.
+constexpr int kMaxLiveChunks = 16;
 template <class F>
 void write_chunks_in_order(FILE *fp, int nchunks, size_t chunk_bytes, int threads, F &&format) {
-  const int nt = std::max(1, threads);
-  std::vector<std::vector<char>> bufs(std::min(nt, nchunks));
-  std::vector<size_t> used(bufs.size());
+  const int nt = std::max(1, std::min({threads, kMaxLiveChunks, nchunks}));
+  std::vector<std::unique_ptr<char[]>> bufs(nt);
+  std::vector<size_t> used(nt);
   for (int c0 = 0; c0 < nchunks; c0 += nt) {
     const int n = std::min(nt, nchunks - c0);
     std::vector<std::thread> pool;
     for (int t = 0; t < n; t++)
       pool.emplace_back([&, t] {
-        bufs[t].resize(chunk_bytes);
-        used[t] = format(c0 + t, bufs[t].data()) - bufs[t].data();
+        if (!bufs[t]) bufs[t].reset(new char[chunk_bytes]);  // default-initialised: no zero fill
+        used[t] = format(c0 + t, bufs[t].get()) - bufs[t].get();
       });
     for (auto &th : pool) th.join();
-    for (int t = 0; t < n; t++) fwrite(bufs[t].data(), 1, used[t], fp);
+    for (int t = 0; t < n; t++) fwrite(bufs[t].get(), 1, used[t], fp);
   }
 }
 
@@ -355,7 +360,7 @@ constexpr size_t kMaxRowBytes = 128;
 void write_cost_log(FILE *fp, const std::vector<ShapeInfo> &shapes, int nctus, int W, const int32_t *cost,
                     const int32_t *sad, const int32_t *satd, int threads) {
   const int ctu_cols = (W + 127) / 128;
-  const int chunk = 8;
+  const int chunk = 2;  // CTUs per chunk: 195 680 rows, <= 25 MB of buffer bound
   const int nchunks = (nctus + chunk - 1) / chunk;
   write_chunks_in_order(fp, nchunks, (size_t)chunk * MIP_COSTS_PER_CTU_ABI * kMaxRowBytes, threads, [&](int c, char *p) {
     for (int ctu = c * chunk; ctu < std::min(nctus, (c + 1) * chunk); ctu++) {

@@ -97,6 +97,15 @@ constexpr int kWeightRows = 768, kWeightRowOffS1 = 384, kWeightRowOffS0 = 512;
 constexpr int kCtabRows = 384 + 4;  // + 4 copies of kAccInitS2 (row 384..387)
 constexpr int kTableBytes = kWeightRows * 16 + kCtabRows * 4;
 
+// One CU searched by the exact per-CU kernel (fixup_kernel): alternative references whose
+// samples may exceed 10 bits (mipgpu.cpp reads_last_columns).
+struct FixupCu {
+  uint32_t ctu;
+  uint16_t cu;     // CU index inside the CTU (reference order, 0..5379)
+  uint8_t shape;
+  uint8_t pad;
+};
+
 struct BestArgs {
   const int32_t *cost;
   uint8_t *best_mode;     // [total_cus][k]
@@ -124,5 +133,8 @@ hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 hipError_t launch_unpack_best(const uint32_t *packed, uint8_t *best_mode, int32_t *best_cost, int total_cus,
                               hipStream_t s);
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s);
+// Exact per-CU search of `n` CUs of every frame (same outputs as the search kernel: cost /
+// SAD / SATD tables or, decisions only, the packed argmin in a.best).
+hipError_t launch_fixup(const SearchArgs &a, const FixupCu *cus, int n, int nframes, hipStream_t s);
 
 }  // namespace mipgpu

@@ -151,34 +151,68 @@ bool cu_defined(int width, int height, int x, int y, int w, int h) {
   return y + h <= height && (long long)(y + h - 1) * width + x + w - 1 < (long long)width * height;
 }
 
-// CTU -> variant (index of the CTU's set of defined CUs), and each variant's first CTU.
+// Reference samples above 10 bits.  At widths that are not multiples of 128 the reference's
+// separable filters give the last one or two frame columns values up to ~1.7 x 1023: the
+// horizontal pass there sums the wrapped next-row samples while the scale is the frame-edge
+// class (intra.cl:3446-3458, 3771-3788).  The search kernel's arithmetic is sized for 10-bit
+// samples, so with alternative references the CUs that read columns W-2 or W-1 (their top
+// row, left column or padding sample) are left to the exact per-CU kernel (fixup_kernel).
+bool reads_last_columns(int width, int height, int x, int y, int w, int h) {
+  (void)height;
+  auto col_hit = [&](long long li) { const long long c = li % width; return c >= width - 2; };
+  if (y > 0) {
+    for (int i = 0; i < w; i++)
+      if (col_hit((long long)(y - 1) * width + x + i)) return true;
+  } else if (x > 0 && col_hit(x - 1)) {
+    return true;
+  }
+  if (x > 0) {
+    for (int i = 0; i < h; i++)
+      if (col_hit((long long)(y + i) * width + x - 1)) return true;
+  } else if (y > 0 && col_hit((long long)(y - 1) * width)) {
+    return true;
+  }
+  return false;
+}
+
+// CTU -> variant = index of the CTU's set of CUs the search kernel computes (the others get
+// MIP_COST_UNAVAILABLE from the fill lists; the fixup kernel overwrites its CUs after).
+// Two maps share the variants: original references ([0]: every defined CU) and alternative
+// references ([1]: minus the fixup CUs when the width is not a multiple of 128).
 struct CtuVariants {
-  std::vector<uint8_t> of_ctu;
-  std::vector<int> rep;
+  std::vector<uint8_t> of_ctu[2];
+  std::vector<std::vector<bool>> pattern;  // [variant][CU in CTU order]
+  std::vector<mipgpu::FixupCu> fixup;      // ALT: CUs computed by the fixup kernel
 };
 
 CtuVariants ctu_variants(int width, int height) {
   CtuVariants v;
   const int cols = (width + 127) / 128, n = cols * ((height + 127) / 128);
-  std::vector<std::vector<bool>> seen;
-  for (int c = 0; c < n; c++) {
-    const int cx = 128 * (c % cols), cy = 128 * (c / cols);
-    std::vector<bool> pat;
-    pat.reserve(MIP_CUS_PER_CTU);
-    for (int s = 0; s < MIP_NUM_SHAPES; s++) {
-      const mip_shape_desc &sd = kShapes[s];
-      for (int cu = 0; cu < sd.ncu; cu++)
-        pat.push_back(cu_defined(width, height, cx + axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols),
-                                 cy + axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols), sd.w, sd.h));
+  for (int alt = 0; alt < 2; alt++)
+    for (int c = 0; c < n; c++) {
+      const int cx = 128 * (c % cols), cy = 128 * (c / cols);
+      // only CTUs whose CUs reach the last columns can hold fixup CUs (wraps: W < 256)
+      const bool near_edge = alt && width % 128 && (cx + 256 >= width || width < 256);
+      std::vector<bool> pat;
+      pat.reserve(MIP_CUS_PER_CTU);
+      int k = 0;
+      for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+        const mip_shape_desc &sd = kShapes[s];
+        for (int cu = 0; cu < sd.ncu; cu++, k++) {
+          const int lx = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), ly = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
+          bool on = cu_defined(width, height, cx + lx, cy + ly, sd.w, sd.h);
+          if (on && near_edge && reads_last_columns(width, height, cx + lx, cy + ly, sd.w, sd.h)) {
+            on = false;
+            v.fixup.push_back(mipgpu::FixupCu{(uint32_t)c, (uint16_t)k, (uint8_t)s, 0});
+          }
+          pat.push_back(on);
+        }
+      }
+      size_t var = 0;
+      while (var < v.pattern.size() && v.pattern[var] != pat) var++;
+      if (var == v.pattern.size()) v.pattern.push_back(pat);
+      v.of_ctu[alt].push_back((uint8_t)std::min<size_t>(var, 255));
     }
-    size_t k = 0;
-    while (k < seen.size() && seen[k] != pat) k++;
-    if (k == seen.size()) {
-      seen.push_back(pat);
-      v.rep.push_back(c);
-    }
-    v.of_ctu.push_back((uint8_t)k);
-  }
   return v;
 }
 
@@ -194,9 +228,9 @@ double pair_cost(int cls, int ncu) {
 WorkLists build_work(int slices, int waves, int width, int height, const CtuVariants &cv) {
   WorkLists wl;
   const int cols = (width + 127) / 128;
-  for (int vq = 0; vq < 4 * (int)cv.rep.size(); vq++) {
+  (void)cols;
+  for (int vq = 0; vq < 4 * (int)cv.pattern.size(); vq++) {
     const int var = vq / 4, q = vq % 4;
-    const int cx = 128 * (cv.rep[var] % cols), cy = 128 * (cv.rep[var] / cols);  // the variant's first CTU
     wl.fill_begin.push_back((int)wl.fill.size());
     struct Piece { mipgpu::WaveTask t; double cost; };
     std::vector<Piece> pieces;
@@ -209,7 +243,7 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
       for (int cu = 0; cu < sd.ncu; cu++) {
         const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
         if (x / 64 != (q & 1) || y / 64 != (q >> 1)) continue;
-        if (!cu_defined(width, height, cx + x, cy + y, sd.w, sd.h)) {
+        if (!cv.pattern[var][shape_cu0 + cu]) {
           const uint32_t off = sd.cost_offset + cu * 2 * sd.modes;  // multiple of 4 entries
           for (uint32_t u = 0; u < (uint32_t)(2 * sd.modes) / 4; u++) wl.fill.push_back(off / 4 + u);
           continue;
@@ -333,7 +367,9 @@ struct mip_engine {
   };
   std::vector<Work> work;
   uint8_t *d_tables = nullptr;
-  uint8_t *d_ctu_var = nullptr;  // [nctus] CTU variant (ctu_variants)
+  uint8_t *d_ctu_var[2] = {nullptr, nullptr};  // [orig / alt refs][nctus] CTU variant (ctu_variants)
+  mipgpu::FixupCu *d_fixup = nullptr;          // alt refs: CUs of the exact per-CU kernel
+  int nfixup = 0;
   int resident[2] = {0, 0};  // persistent search grid (workgroups resident on this device), [alt]
   // Engine-owned reference scratch d_refs, written by the engine filter when a device-API
   // search has no caller references: every such search records refs_done on its stream, and
@@ -429,7 +465,7 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream3) (void)hipStreamSynchronize(e->stream3);
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables,
-                  (void *)e->d_ctu_var})
+                  (void *)e->d_ctu_var[0], (void *)e->d_ctu_var[1], (void *)e->d_fixup})
     if (p) (void)hipFree(p);
   if (e->d_queue) (void)hipFree(e->d_queue);
   for (hipEvent_t ev : e->queue_done)
@@ -522,10 +558,20 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
   const CtuVariants cv = ctu_variants(width, height);
-  if (cv.rep.size() > (size_t)mipgpu::kMaxCtuVariants) return cleanup(fail("too many CTU variants (%zu)", cv.rep.size()));
-  ALLOC(e->d_ctu_var, cv.of_ctu.size());
-  if (hipMemcpy(e->d_ctu_var, cv.of_ctu.data(), cv.of_ctu.size(), hipMemcpyHostToDevice) != hipSuccess)
-    return cleanup(fail("uploading CTU variants failed"));
+  if (cv.pattern.size() > (size_t)mipgpu::kMaxCtuVariants)
+    return cleanup(fail("too many CTU variants (%zu)", cv.pattern.size()));
+  for (int alt = 0; alt < 2; alt++) {
+    ALLOC(e->d_ctu_var[alt], cv.of_ctu[alt].size());
+    if (hipMemcpy(e->d_ctu_var[alt], cv.of_ctu[alt].data(), cv.of_ctu[alt].size(), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail("uploading CTU variants failed"));
+  }
+  e->nfixup = (int)cv.fixup.size();
+  if (e->nfixup) {
+    ALLOC(e->d_fixup, cv.fixup.size() * sizeof(mipgpu::FixupCu));
+    if (hipMemcpy(e->d_fixup, cv.fixup.data(), cv.fixup.size() * sizeof(mipgpu::FixupCu), hipMemcpyHostToDevice) !=
+        hipSuccess)
+      return cleanup(fail("uploading fixup CUs failed"));
+  }
   std::vector<int> slice_set;
   if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
   else slice_set = {1, 2, 4};
@@ -623,7 +669,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.fill = work.d_fill;
   a.fill_begin = work.d_fill_begin;
   a.tables = reinterpret_cast<const uint4 *>(e->d_tables);
-  a.ctu_var = e->d_ctu_var;
+  a.ctu_var = e->d_ctu_var[alt ? 1 : 0];
   a.width = e->width;
   a.height = e->height;
   a.ctu_cols = e->ctu_cols;
@@ -661,6 +707,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   if (e->queue_used[slot]) HIP_TRY(hipStreamWaitEvent(s, e->queue_done[slot], 0));
   a.queue = e->d_queue + 2 * slot;
   HIP_TRY(mipgpu::launch_search(a, nframes, alt, e->resident[alt ? 1 : 0], s));
+  if (alt && e->nfixup) HIP_TRY(mipgpu::launch_fixup(a, e->d_fixup, e->nfixup, nframes, s));
   HIP_TRY(hipEventRecord(e->queue_done[slot], s));
   e->queue_used[slot] = true;
   if (engine_refs) {
