@@ -369,6 +369,20 @@ def test_async_host_calls_in_flight(gpu_available):
     assert np.array_equal(o4["cost"][0], O.search(frames[8]))
 
 
+def test_dropped_ticket_waits(gpu_available):
+    """A search_async ticket dropped without wait(): its finaliser waits, so the output and
+    input arrays it keeps alive are not freed while the engine's copies use them; the
+    engine stays usable."""
+    import gc
+    w, h = 256, 136
+    frames = synth_frames(w, h, 4, 0xD70, 0)
+    with MipEngine(w, h, max_batch=2) as eng:
+        for _ in range(3):
+            eng.search_async(frames)  # dropped at once
+        gc.collect()
+        assert np.array_equal(eng.search(frames[1])["cost"][0], O.search(frames[1]))
+
+
 def test_async_host_calls_and_device_filter_scratch(gpu_available):
     """An engine with a filter: asynchronous host calls (filtering into the reference
     scratch per slot) in flight while a device-API search filters into the same scratch on

@@ -16,6 +16,7 @@
 
 #include "mip_kernels.h"
 #include "mip_tables.h"
+#include "queue_ring.h"
 
 namespace {
 
@@ -383,8 +384,15 @@ struct mip_engine {
   static constexpr int kQueueSlots = 16;
   uint32_t *d_queue = nullptr;
   hipEvent_t queue_done[kQueueSlots] = {};
-  bool queue_used[kQueueSlots] = {};
-  unsigned queue_seq = 0;
+  struct QueueOps {
+    mip_engine *e;
+    int wait(int slot, hipStream_t s) const { return hipStreamWaitEvent(s, e->queue_done[slot], 0) != hipSuccess; }
+    int record(int slot, hipStream_t s) const { return hipEventRecord(e->queue_done[slot], s) != hipSuccess; }
+    int clear(int slot, hipStream_t s) const {
+      return hipMemsetAsync(e->d_queue + 2 * slot, 0, 2 * sizeof(uint32_t), s) != hipSuccess;
+    }
+  };
+  QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this}};
 };
 
 namespace {
@@ -703,13 +711,16 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     }
   }
   if (decisions_only) HIP_TRY(hipMemsetAsync(d_best_cost, 0xff, (size_t)total_cus * 4, s));
-  const int slot = (int)(e->queue_seq++ % mip_engine::kQueueSlots);
-  if (e->queue_used[slot]) HIP_TRY(hipStreamWaitEvent(s, e->queue_done[slot], 0));
+  const int slot = e->queue.acquire(s);
+  if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + 2 * slot;
-  HIP_TRY(mipgpu::launch_search(a, nframes, alt, e->resident[alt ? 1 : 0], s));
+  const hipError_t le = mipgpu::launch_search(a, nframes, alt, e->resident[alt ? 1 : 0], s);
+  if (le != hipSuccess) {
+    e->queue.failed(slot);  // the pair is cleared before its next use
+    return fail("search launch failed: %s", hipGetErrorString(le));
+  }
+  if (e->queue.launched(slot, s) != 0) return fail("hipEventRecord failed");
   if (alt && e->nfixup) HIP_TRY(mipgpu::launch_fixup(a, e->d_fixup, e->nfixup, nframes, s));
-  HIP_TRY(hipEventRecord(e->queue_done[slot], s));
-  e->queue_used[slot] = true;
   if (engine_refs) {
     HIP_TRY(hipEventRecord(e->refs_done, s));
     e->refs_pending = true;
@@ -746,10 +757,16 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
                             void *stream) {
   if (!e) return fail("engine is NULL");
   if (!d_costs) return fail("d_costs is NULL");
+  // an empty range (more CTU-row bands than CTU rows, mipgpu.split) is a successful no-op
+  if (ctu_begin == ctu_end && ctu_begin >= 0 && ctu_end <= e->nctus) return 0;
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, nullptr, nullptr,
                             (hipStream_t)stream, ctu_begin, ctu_end - ctu_begin);
 }
+
+static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
+                                int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
+                                int32_t *satd_out);
 
 int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                             int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
@@ -758,6 +775,34 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
   *ticket = 0;
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
   HIP_TRY(hipSetDevice(e->device));
+  const int rc = search_frames_chunks(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out,
+                                      sad_out, satd_out);
+  // Also after a failure part-way through the chunks: the chunks already queued on the
+  // upload / search streams are covered by host_done (later device-API searches that filter
+  // into the engine's reference scratch wait for it) and by this call's completion event.
+  const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
+  if (hipEventRecord(e->host_done, e->stream) != hipSuccess) return rc ? rc : fail("hipEventRecord failed");
+  e->host_pending = true;
+  if (rc != 0) {
+    const std::string err = g_err;
+    (void)hipStreamSynchronize(e->stream2);
+    (void)hipStreamSynchronize(e->stream);
+    (void)hipStreamSynchronize(e->stream3);
+    g_err = err;
+    return rc;
+  }
+  // completion on the download stream, after this call's search and every earlier call's
+  // downloads: calls complete in order
+  if (!any_out) HIP_TRY(hipStreamWaitEvent(e->stream3, e->host_done, 0));
+  const uint64_t call = ++e->host_calls;
+  HIP_TRY(hipEventRecord(e->call_done[(call - 1) % mip_engine::kCallRing], e->stream3));
+  *ticket = call;
+  return 0;
+}
+
+static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
+                                int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
+                                int32_t *satd_out) {
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
     HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
@@ -821,14 +866,6 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
       HIP_TRY(hipMemcpyAsync(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, hipMemcpyDeviceToHost, down));
     HIP_TRY(hipEventRecord(e->slot_down[sl], down));
   }
-  HIP_TRY(hipEventRecord(e->host_done, comp));
-  e->host_pending = true;
-  // completion on the download stream, after this call's search and every earlier call's
-  // downloads: calls complete in order
-  if (!any_out) HIP_TRY(hipStreamWaitEvent(down, e->host_done, 0));
-  const uint64_t call = ++e->host_calls;
-  HIP_TRY(hipEventRecord(e->call_done[(call - 1) % mip_engine::kCallRing], down));
-  *ticket = call;
   return 0;
 }
 

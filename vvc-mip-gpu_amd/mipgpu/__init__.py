@@ -129,10 +129,20 @@ def pinned_empty(shape, dtype) -> np.ndarray:
 
 class _Ticket:
     """An asynchronous host search in flight: its number, its outputs, and its inputs (kept
-    alive until the search has completed)."""
+    alive until the search has completed).  A ticket dropped without wait() waits in its
+    finaliser, so numpy never frees arrays the engine's copies may still be using."""
 
-    def __init__(self, value, out, keep):
-        self.value, self.out, self._keep = value, out, keep
+    def __init__(self, value, out, keep, engine=None):
+        self.value, self.out, self._keep, self._engine = value, out, keep, engine
+        self.done = engine is None
+
+    def __del__(self):
+        eng = getattr(self, "_engine", None)
+        if not getattr(self, "done", True) and eng is not None and getattr(eng, "_h", None):
+            try:
+                library().mip_wait(eng._h, ctypes.c_uint64(self.value))
+            except Exception:
+                pass
 
 
 class MipEngine:
@@ -157,7 +167,7 @@ class MipEngine:
 
     def close(self):
         if getattr(self, "_h", None):
-            library().mip_engine_destroy(self._h)
+            library().mip_engine_destroy(self._h)  # synchronises the engine streams first
             self._h = None
 
     def __del__(self):
@@ -230,11 +240,12 @@ class MipEngine:
         _check(library().mip_search_frames_async(self._h, _ptr(f), _ptr(r), n, _ptr(res.get("cost")),
                                                  _ptr(res.get("best_mode")), _ptr(res.get("best_cost")),
                                                  _ptr(res.get("sad")), _ptr(res.get("satd")), ctypes.byref(t)))
-        return _Ticket(t.value, res, (f, r))
+        return _Ticket(t.value, res, (f, r), self)
 
     def wait(self, ticket):
         """Block until an asynchronous search has completed; returns its output dict."""
         _check(library().mip_wait(self._h, ctypes.c_uint64(ticket.value)))
+        ticket.done = True
         return ticket.out
 
     def filter_frames(self, frames, filter, kernel_idx=0):
