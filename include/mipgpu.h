@@ -19,8 +19,11 @@
  * Cost layout (identical to the reference's ALL_stridedDistortionsPerCtu,
  * constants.h:1558-1631): int32 [frames][nCTUs][97840], entry
  *     ctu*97840 + shape_offset + cu*2*modes + mode
- * with the 47 CU shapes in reference order.  CUs that do not lie completely inside the
- * frame are reported as MIP_COST_UNAVAILABLE (the reference leaves them undefined).
+ * with the 47 CU shapes in reference order.  Samples are addressed like the reference does,
+ * by linear index y * width + x, so CUs right of the frame (widths that are not multiples
+ * of 128) read the next row's samples and get the reference's costs.  CUs whose cost the
+ * reference leaves undefined -- below the frame (stale LDS, intra.cl:96-98) or reading past
+ * the frame's end -- are reported as MIP_COST_UNAVAILABLE.
  */
 #ifndef MIPGPU_H
 #define MIPGPU_H
@@ -31,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MIPGPU_ABI_VERSION 4
+#define MIPGPU_ABI_VERSION 5
 #define MIP_COSTS_PER_CTU_ABI 97840
 #define MIP_CUS_PER_CTU_ABI 5380
 #define MIP_COST_UNAVAILABLE 0x7fffffff
@@ -160,6 +163,17 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
  * device time per launch in milliseconds (HIP events on that stream), or <0. */
 double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
                               int nframes, int32_t *d_costs, int reps);
+
+/* Per-frame device times of the host pipeline, for the reference's stdout report
+ * ("FilterSamples took %f ms" and the filter TIMING REPORT, main.cpp:749-775; the frame
+ * write time, main.cpp:580-595).  mip_trace_times(e, 1): mip_search_frames[_async] brackets
+ * every chunk's upload and filter launch with HIP timing events (a buffer slot is then reused
+ * only after its times were read: tracing costs some overlap).  mip_pop_times returns the
+ * per-frame times (the chunk's time / its frames, frame order) of the calls completed so
+ * far: up to `max` frames into upload_ms / filter_ms (either may be NULL; filter 0 without
+ * a filter), the count in *n. */
+int mip_trace_times(mip_engine *e, int enable);
+int mip_pop_times(mip_engine *e, double *upload_ms, double *filter_ms, int max, int *n);
 
 /* Page-locked host memory (hipHostMalloc): host buffers for mip_search_frames /
  * mip_filter_frames allocated here are transferred by DMA at full PCIe rate (pageable

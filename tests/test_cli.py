@@ -101,6 +101,20 @@ def test_extension_arguments_are_validated():
     assert all(k in r.stdout for k in ("--TopK", "--BinaryLog", "--InputFormat"))
 
 
+@needs_cli
+@pytest.mark.parametrize("args,size", [([], "130x64"), (["--StrictResolution"], "640x480")])
+def test_unsupported_resolution_message(tmp_path, args, size):
+    """main.cpp:301-309: an unsupported size prints the reference's error and its resolution
+    table, and exits 0 (sizes not multiples of 4; with --StrictResolution every size outside
+    the reference's table)."""
+    r = run(["-f", "1", "-s", size, "-o", str(tmp_path / "none.csv")] + args)
+    assert r.returncode == 0
+    assert f"[!] ERROR: Unsupported resolution {size}\nSupported resolutions are:\n" in r.stdout
+    for res in ("3840x2160", "1920x1080", "1280x720", "832x480", "416x240"):
+        assert f"  {res}\n" in r.stdout
+    assert "Current frame" not in r.stdout
+
+
 # ------------------------------------------------------------ GPU: the cost log
 @pytest.mark.gpu
 @needs_cli
@@ -141,6 +155,14 @@ def test_cost_log_is_byte_identical(gpu_available, tmp_path, extra, filt, kidx, 
     assert r.returncode == 0, r.stdout + r.stderr
     for f in range(N):
         assert f"Current frame {f}\n" in r.stdout
+    # the reference's per-frame report: stages (fused here) and, with a filter, its device time
+    stages = ("Performing initBoundaries kernel...\nPerforming MIP_ReducedPred kernel...\n" +
+              "Performing upsampleDistortion kernel...\n" * 3)
+    assert r.stdout.count(stages) == N
+    took = re.findall(r"FilterSamples took ([0-9.]+) ms\n\nTIMING REPORT\nWrite\(ns\): [0-9.]+\nExecution\(ns\):([0-9.]+)\n"
+                      r"Read\(ns\): 0.000000\nTotalFilterTime\(ms\): [0-9.]+\n", r.stdout)
+    assert len(took) == (N if filt else 0)
+    assert all(float(ms) > 0 and abs(float(ms) * 1e6 - float(ns)) < 1 for ms, ns in took)
     assert re.search(rf"Elapsed time \(ms\) from writing samples to reading distortion \({N}x\), \d+\n", r.stdout)
     refs = None if filt is None else O.filter_frame(frames[0], filt, kidx)
     res = O.search(frames[0], refs, want_sad_satd=sad_satd)

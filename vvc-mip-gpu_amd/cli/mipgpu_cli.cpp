@@ -55,7 +55,7 @@ struct Options {
   std::vector<int> devices{0};
   std::string device_arg = "0";
   bool device_set = false, prefix_set = false, kidx_set = false, help = false;
-  bool sad_satd = false, all_frames = false;
+  bool sad_satd = false, all_frames = false, strict_res = false;
   std::string resolution, input, prefix, filter, best_modes, binary_log, input_format = "auto";
 };
 
@@ -69,7 +69,7 @@ const OptDef kOpts[] = {{"help", 'h', false},        {"DeviceIndex", 0, true},  
                         {"FilterType", 0, true},     {"KernelIdx", 0, true},     {"ReportSadSatd", 0, false},
                         {"AllFrames", 0, false},     {"BestModes", 0, true},     {"BatchFrames", 0, true},
                         {"Threads", 0, true},        {"TopK", 0, true},          {"BinaryLog", 0, true},
-                        {"InputFormat", 0, true}};
+                        {"InputFormat", 0, true},    {"StrictResolution", 0, false}};
 
 void usage() {
   std::cout << "Allowed options:\n"
@@ -88,7 +88,8 @@ void usage() {
                "  --Threads arg (=0)                CSV parsing / log-formatting threads (0 = all cores)\n"
                "  --TopK arg (=1)                   Modes per CU in the BestModes file (1..32, ranked)\n"
                "  --BinaryLog arg                   Write every frame's int32 cost table to this file\n"
-               "  --InputFormat arg (=auto)         csv | u16 (raw 16-bit luma) | yuv420p10 (planar 4:2:0, 10 bit)\n";
+               "  --InputFormat arg (=auto)         csv | u16 (raw 16-bit luma) | yuv420p10 (planar 4:2:0, 10 bit)\n"
+               "  --StrictResolution                Accept only the reference's resolutions (constants.h:17-23)\n";
 }
 
 int set_opt(Options &o, const std::string &name, const std::string &val) {
@@ -111,6 +112,7 @@ int set_opt(Options &o, const std::string &name, const std::string &val) {
     else if (name == "KernelIdx") o.kernel_idx = std::stoi(val), o.kidx_set = true;
     else if (name == "ReportSadSatd") o.sad_satd = true;
     else if (name == "AllFrames") o.all_frames = true;
+    else if (name == "StrictResolution") o.strict_res = true;
     else if (name == "BestModes") o.best_modes = val;
     else if (name == "BatchFrames") o.batch = std::max(1, std::stoi(val));
     else if (name == "Threads") o.threads = std::stoi(val);
@@ -449,6 +451,18 @@ int main(int argc, char **argv) {
     std::cout << "  [!] ERROR: Input resolution \"" << o.resolution << "\" not set properly" << std::endl;
     return 0;
   }
+  // The reference's resolution table (constants.h:17-23, main.cpp:301-309).  This engine also
+  // takes every other size that is a multiple of 4 unless --StrictResolution is given.
+  static const int kRefRes[5][2] = {{3840, 2160}, {1920, 1080}, {1280, 720}, {832, 480}, {416, 240}};
+  bool listed = false;
+  for (const auto &r : kRefRes) listed = listed || (r[0] == W && r[1] == H);
+  if ((o.strict_res && !listed) || W % 4 || H % 4) {
+    printf("[!] ERROR: Unsupported resolution %dx%d\n", W, H);
+    printf("Supported resolutions are:\n");
+    for (const auto &r : kRefRes) printf("  %dx%d\n", r[0], r[1]);
+    if (!o.strict_res) printf("  (and any other width x height that are multiples of 4)\n");
+    return 0;
+  }
   const std::string fmt = input_format(o);
   const int threads = o.threads > 0 ? o.threads : (int)std::max(1u, std::thread::hardware_concurrency());
   FrameSource src;
@@ -477,6 +491,11 @@ int main(int argc, char **argv) {
       return 1;
     }
     engines.push_back(e);
+    if (filter != MIP_FILTER_NONE && mip_trace_times(e, 1) != 0) {
+      std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
+      destroy_all();
+      return 1;
+    }
   }
   const int ndev = (int)engines.size();
   const size_t fs = (size_t)W * H;
@@ -607,6 +626,7 @@ int main(int argc, char **argv) {
   // 908-914): the summed wall time of the chunks' device round trips (H2D, search, D2H);
   // file reading and log writing, outside that window in the reference, overlap it here.
   std::chrono::steady_clock::duration search_time{};
+  double write_ns = 0;  // the reference's writeTime_filter
   std::vector<int> rcs(ndev, 0);
   std::vector<std::string> errs(ndev);
   for (int c = 0; c < nchunks && !search_failed; c++) {
@@ -654,7 +674,36 @@ int main(int argc, char **argv) {
         fail(search_failed);
       }
     if (search_failed) break;
-    for (int i = 0; i < n; i++) std::cout << "Current frame " << f0 + i << std::endl;
+    // The reference's per-frame report (main.cpp:681, 709, 754, 771-775, 804, 911, 997,
+    // 1076, 1153): the frame number, with alternative references the filter's device time,
+    // and the stages -- boundaries, reduced prediction, upsampling + distortion -- which run
+    // fused in one search launch here.
+    std::vector<double> up_ms(n, 0.0), filt_ms(n, 0.0);
+    if (filter != MIP_FILTER_NONE) {
+      int got = 0;
+      for (int d = 0; d < ndev; d++) {
+        int k = 0;
+        if (mip_pop_times(engines[d], up_ms.data() + got, filt_ms.data() + got, n - got, &k) == 0) got += k;
+      }
+      if (c == 0) write_ns = up_ms[0] * 1e6;  // writeTime_filter: the first frame's upload (main.cpp:580-595)
+    }
+    for (int i = 0; i < n; i++) {
+      printf("Current frame %d\n", f0 + i);
+      if (filter != MIP_FILTER_NONE) {
+        const double exec_ns = filt_ms[i] * 1e6;
+        printf("Performing filterFrame kernel...\n");
+        printf("FilterSamples took %f ms\n\n", exec_ns / 1000000);
+        printf("TIMING REPORT\n");
+        printf("Write(ns): %f\n", write_ns);
+        printf("Execution(ns):%f\n", exec_ns);
+        printf("Read(ns): %f\n", 0.0);
+        printf("TotalFilterTime(ms): %f\n", (write_ns + exec_ns) / 1000000);
+      }
+      printf("Performing initBoundaries kernel...\n");
+      printf("Performing MIP_ReducedPred kernel...\n");
+      for (int u = 0; u < 3; u++) printf("Performing upsampleDistortion kernel...\n");
+    }
+    fflush(stdout);
     set_state(s, 2);
   }
   reader.join();

@@ -353,6 +353,14 @@ struct mip_engine {
   // engine's reference scratch wait for it (the host pipeline uses the same buffer).
   hipEvent_t host_done = nullptr;
   bool host_pending = false;
+  // mip_trace_times: per-slot timing events around the chunk's upload and filter launch,
+  // the chunk (sequence number, frames) whose events are pending, and the per-frame times
+  // read so far.
+  bool trace = false;
+  hipEvent_t tr_ev[kHostSlots][4] = {};  // upload start / end, filter start / end
+  uint64_t tr_chunk[kHostSlots] = {};
+  int tr_frames[kHostSlots] = {}, tr_filter[kHostSlots] = {};
+  std::vector<std::pair<double, double>> tr_times;
   uint16_t *d_frames = nullptr, *d_refs = nullptr;
   int32_t *d_costs = nullptr, *d_sad = nullptr, *d_satd = nullptr, *d_best_cost = nullptr;
   uint8_t *d_best = nullptr;
@@ -485,6 +493,9 @@ int mip_engine_destroy(mip_engine *e) {
   for (hipEvent_t ev : e->call_done)
     if (ev) (void)hipEventDestroy(ev);
   if (e->host_done) (void)hipEventDestroy(e->host_done);
+  for (auto &evs : e->tr_ev)
+    for (hipEvent_t ev : evs)
+      if (ev) (void)hipEventDestroy(ev);
   for (const mip_engine::Work &w : e->work)
     for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin})
       if (p) (void)hipFree(p);
@@ -768,6 +779,22 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
                                 int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
                                 int32_t *satd_out);
 
+// mip_trace_times: read the pending chunk times of slot `sl` (waits for its events).
+static int drain_trace(mip_engine *e, int sl) {
+  if (!e->tr_frames[sl]) return 0;
+  float up = 0, fl = 0;
+  HIP_TRY(hipEventSynchronize(e->tr_ev[sl][1]));
+  HIP_TRY(hipEventElapsedTime(&up, e->tr_ev[sl][0], e->tr_ev[sl][1]));
+  if (e->tr_filter[sl]) {
+    HIP_TRY(hipEventSynchronize(e->tr_ev[sl][3]));
+    HIP_TRY(hipEventElapsedTime(&fl, e->tr_ev[sl][2], e->tr_ev[sl][3]));
+  }
+  const int n = e->tr_frames[sl];
+  for (int i = 0; i < n; i++) e->tr_times.push_back({(double)up / n, (double)fl / n});
+  e->tr_frames[sl] = 0;
+  return 0;
+}
+
 int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                             int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
                             int32_t *satd_out, uint64_t *ticket) {
@@ -831,7 +858,12 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     const size_t fo = (size_t)sl * sb;  // first engine frame slot of this chunk
     uint16_t *d_frames = e->d_frames + fo * fs;
     if (reuse) HIP_TRY(hipStreamWaitEvent(up, e->slot_comp[sl], 0));
+    if (e->trace) {
+      if (drain_trace(e, sl) != 0) return -1;
+      HIP_TRY(hipEventRecord(e->tr_ev[sl][0], up));
+    }
     HIP_TRY(hipMemcpyAsync(d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, up));
+    if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][1], up));
     const uint16_t *d_refs = nullptr;
     if (refs_or_null) {
       HIP_TRY(hipMemcpyAsync(e->d_refs + fo * fs, refs_or_null + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, up));
@@ -840,11 +872,19 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     HIP_TRY(hipEventRecord(e->slot_up[sl], up));
     HIP_TRY(hipStreamWaitEvent(comp, e->slot_up[sl], 0));
     if (reuse) HIP_TRY(hipStreamWaitEvent(comp, e->slot_down[sl], 0));
-    if (!refs_or_null && e->opts.filter != MIP_FILTER_NONE) {
+    const bool filt = !refs_or_null && e->opts.filter != MIP_FILTER_NONE;
+    if (filt) {
+      if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][2], comp));
       if (mip_filter_device(d_frames, e->d_refs + fo * fs, e->width, e->height, nb, e->opts.filter,
                             e->opts.kernel_idx, comp) != 0)
         return -1;
+      if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][3], comp));
       d_refs = e->d_refs + fo * fs;
+    }
+    if (e->trace) {
+      e->tr_frames[sl] = nb;
+      e->tr_filter[sl] = filt;
+      e->tr_chunk[sl] = k;
     }
     // decisions only (no cost / SAD / SATD table requested, K = 1): the fused argmin, no table
     const bool decisions_only = !costs_out && !sad_out && !satd_out && e->opts.best_k == 1 &&
@@ -887,6 +927,36 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
                               satd_out, &ticket) != 0)
     return -1;
   return mip_wait(e, ticket);
+}
+
+int mip_trace_times(mip_engine *e, int enable) {
+  if (!e) return fail("engine is NULL");
+  HIP_TRY(hipSetDevice(e->device));
+  if (enable && !e->tr_ev[0][0])
+    for (auto &evs : e->tr_ev)
+      for (hipEvent_t &ev : evs) HIP_TRY(hipEventCreate(&ev));
+  e->trace = enable != 0;
+  return 0;
+}
+
+int mip_pop_times(mip_engine *e, double *upload_ms, double *filter_ms, int max, int *n) {
+  if (!e || !n || max < 0) return fail("bad arguments");
+  HIP_TRY(hipSetDevice(e->device));
+  // pending chunks in sequence order (frame order)
+  std::vector<int> order;
+  for (int sl = 0; sl < mip_engine::kHostSlots; sl++)
+    if (e->tr_frames[sl]) order.push_back(sl);
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return e->tr_chunk[a] < e->tr_chunk[b]; });
+  for (int sl : order)
+    if (drain_trace(e, sl) != 0) return -1;
+  const int k = std::min<int>(max, (int)e->tr_times.size());
+  for (int i = 0; i < k; i++) {
+    if (upload_ms) upload_ms[i] = e->tr_times[i].first;
+    if (filter_ms) filter_ms[i] = e->tr_times[i].second;
+  }
+  e->tr_times.erase(e->tr_times.begin(), e->tr_times.begin() + k);
+  *n = k;
+  return 0;
 }
 
 int mip_host_alloc(size_t bytes, void **out) {
