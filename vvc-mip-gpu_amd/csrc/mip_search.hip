@@ -78,6 +78,9 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #ifndef MIP_WIN_UNROLL
 #define MIP_WIN_UNROLL 2  // windows of the vertical pass per loop iteration (A/B knob)
 #endif
+#ifndef MIP_PAIR_BLOCKS
+#define MIP_PAIR_BLOCKS 1  // classes with an even block count per lane walk block pairs (A/B knob)
+#endif
 #ifndef MIP_ONLY_CLASS
 #define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
 #endif
@@ -363,6 +366,88 @@ __device__ __forceinline__ void block_finish(const BlockAcc &b, u2 &sad, u2 &sat
   sad = as_u2(as_s2(b.pos + b.pos) - dc);
 }
 
+// ---- paired blocks ---------------------------------------------------------------------
+// Classes whose lanes walk an even number of 4x4 blocks per mode pair (H >= 8) process two
+// blocks of the strip at once -- A = rows r..r+3, B = rows r+4..r+7 -- and, per mode, keep the
+// two blocks in the two 16-bit halves of a register (the unpaired path keeps the two modes
+// there).  Sums over the two halves then belong to one mode, so the absolute values of the
+// SATD coefficients and of the SAD residuals are single v_sad_u16 instructions accumulating
+// straight into 32-bit per-mode sums:
+//   |x - y| = sad(x', y') for two values sharing a bias, |x + y| = sad(x', 2b - y'),
+// replacing the unpaired path's max/min folds, packed positive-part sums and unpacking dot2s.
+// The residual rows are computed as before (both modes packed) and transposed once per row
+// (two v_perm_b32 per column).  The per-block SATD rounding (kernel_aux_functions.cl:238-246)
+//   satd_b = (S_b + (|c0| >> 2) + 1) >> 1,  S_b = sum of the 15 non-DC |c_k|,
+// is exact on the pair's sum because S_b and |c0| have the same parity (the 16 coefficients
+// sum to 16 d_0, so sum |c_k| is even): satd_b = (S_b + D_b) / 2 with
+// D_b = (|c0| >> 2) + ((|c0| + (|c0| >> 2)) & 1), and the lane accumulates S_b + D_b (even)
+// over its blocks; the CU's SATD is that sum / 2.
+struct PairAcc {
+  uint32_t sad0 = 0, sad1 = 0;  // per-mode SAD
+  uint32_t t0 = 0, t1 = 0;      // per-mode 2 * SATD
+};
+
+// Biased residual row I of one block, both modes packed (as block_row).
+template <int I>
+__device__ __forceinline__ void residual_row(const s2 (&prow)[4], uint2 orow, uint32_t (&d)[4]) {
+  const s2 o01 = as_s2(orow.x), o23 = as_s2(orow.y);
+  d[0] = as_u32(s2{o01.x, o01.x} - prow[0]);
+  d[1] = as_u32(s2{o01.y, o01.y} - prow[1]);
+  d[2] = as_u32(s2{o23.x, o23.x} - prow[2]);
+  d[3] = as_u32(s2{o23.y, o23.y} - prow[3]);
+}
+
+// Row I of block B: transpose with block A's row I into per-mode (A, B) registers, SAD, row
+// butterflies (carry-free 32-bit adds on the biased values, as block_row).
+template <int I>
+__device__ __forceinline__ void pair_row(const uint32_t *dA, const uint32_t (&dB)[4], uint32_t (&t0)[16],
+                                         uint32_t (&t1)[16], PairAcc &acc) {
+  constexpr const uint32_t *B = kBiasD[I & 1];
+  uint32_t m0[4], m1[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    m0[c] = __builtin_amdgcn_perm(dB[c], dA[c], 0x05040100u);  // (A.mode0, B.mode0)
+    m1[c] = __builtin_amdgcn_perm(dB[c], dA[c], 0x07060302u);  // (A.mode1, B.mode1)
+    acc.sad0 = __builtin_amdgcn_sad_u16(m0[c], splat32(B[c]), acc.sad0);  // |d| = |d' - bias|
+    acc.sad1 = __builtin_amdgcn_sad_u16(m1[c], splat32(B[c]), acc.sad1);
+  }
+  auto rowbf = [&](const uint32_t (&m)[4], uint32_t (&t)[16]) {
+    const uint32_t s0 = m[0] + m[1], s1 = m[0] - m[1], s2_ = m[2] + m[3], s3 = m[2] - m[3];
+    t[4 * I + 0] = s0 + s2_;
+    t[4 * I + 1] = s1 + s3;
+    t[4 * I + 2] = s0 - s2_;
+    t[4 * I + 3] = s1 - s3;
+  };
+  rowbf(m0, t0);
+  rowbf(m1, t1);
+}
+
+// Column butterflies and magnitudes of one mode's block pair (halves = blocks A, B):
+// T += sum over both blocks of S_b + D_b (see above).  Column stage values u0/u2 of column c
+// carry kBiasP[c], u1/u3 kBiasQ (block_finish); 2 * bias - u' = bias - u stays in [0, 65536).
+__device__ __forceinline__ uint32_t pair_finish(const uint32_t (&t)[16], uint32_t T) {
+  static_for<4>([&](auto c_c) {
+    constexpr int c = decltype(c_c)::value;
+    const uint32_t u0 = t[c] + t[4 + c], u1 = t[c] - t[4 + c];
+    const uint32_t u2_ = t[8 + c] + t[12 + c], u3 = t[8 + c] - t[12 + c];
+    const uint32_t n2 = splat32(2 * kBiasP[c]) - u2_, n3 = splat32(2 * kBiasQ) - u3;
+    T = __builtin_amdgcn_sad_u16(u0, u2_, T);  // |u0 - u2|
+    T = __builtin_amdgcn_sad_u16(u1, u3, T);   // |u1 - u3|
+    T = __builtin_amdgcn_sad_u16(u1, n3, T);   // |u1 + u3|
+    if constexpr (c > 0) {
+      T = __builtin_amdgcn_sad_u16(u0, n2, T);  // |u0 + u2|
+    } else {
+      // DC c0 = u0 + u2: |c0| per block = max(u0', n2) - min(u0', n2), then D_b
+      const u2 mx = __builtin_elementwise_max(as_u2(u0), as_u2(n2)), mn = __builtin_elementwise_min(as_u2(u0), as_u2(n2));
+      const uint32_t a = as_u32(mx) - as_u32(mn);
+      const uint32_t q = as_u32(as_u2(a) >> (u2){2, 2});
+      const uint32_t d = q + ((a + q) & 0x00010001u);
+      T = __builtin_amdgcn_sad_u16(d, 0u, T);  // both halves
+    }
+  });
+  return T;
+}
+
 // Packed block results -> 32-bit per-mode accumulators.
 struct Acc {
   uint32_t sad0 = 0, sad1 = 0, satd0 = 0, satd1 = 0;
@@ -618,6 +703,94 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
   }
 }
 
+// Paired walk (see PairAcc): the lane's blocks in [k0, k0 + windows) two at a time, rows
+// generated exactly as in walk_strip; block A's residual rows wait for block B's.
+template <int W, int H, int V>
+constexpr bool kPaired = Geo<W, H, V>::SID != 0 && W * H > 32 && V == kClassV[size_class(W, H)] &&
+                         ((Geo<W, H, V>::CHUNKED ? 4 * Geo<W, H, V>::UV : Geo<W, H, V>::KV * Geo<W, H, V>::UV) / 4) % 2 == 0;
+
+template <int W, int H, int V, class RED>
+__device__ __forceinline__ void walk_pairs(const OrigRows<H> &orig, const RED &red, int x0, int k0, s2 (&prev)[4],
+                                           PairAcc &acc) {
+  using G = Geo<W, H, V>;
+  constexpr int ROWS = G::CHUNKED ? 4 * G::UV : G::KV * G::UV;  // CU rows of this call
+  constexpr int NBP = ROWS / 8;                                   // block pairs
+  const int y0 = k0 * G::UV;                                      // first CU row
+  // per block pair: 4 rows of A -> dA, 4 rows of B -> pair_row
+#pragma unroll 1
+  for (int bp = 0; bp < NBP; bp++) {
+    uint32_t dA[16], t0[16], t1[16];
+    const int yb = y0 + 8 * bp;  // CU row of A's first row
+    // emit(i, prow): CU row yb + i (i = 0..7)
+    auto emit = [&](auto i_c, const s2 (&prow)[4]) {
+      constexpr int i = decltype(i_c)::value;
+      if constexpr (i < 4) {
+        uint32_t d[4];
+        residual_row<i>(prow, orig(yb + i), d);
+#pragma unroll
+        for (int c = 0; c < 4; c++) dA[4 * i + c] = d[c];
+      } else {
+        uint32_t dB[4];
+        residual_row<i - 4>(prow, orig(yb + i), dB);
+        pair_row<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
+      }
+    };
+    if constexpr (G::UV == 1) {
+      static_for<8>([&](auto i_c) {
+        s2 prow[4];
+        anchor_row<W, H>(red, yb + decltype(i_c)::value, x0, prow);
+        emit(i_c, prow);
+      });
+    } else if constexpr (G::UV == 2) {
+      const int kb = yb / 2;  // windows kb..kb+3
+      static_for<4>([&](auto w_c) {
+        constexpr int w = decltype(w_c)::value;
+        s2 next[4], mid[4];
+        anchor_row<W, H>(red, kb + w, x0, next);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) mid[cc] = avg_round(prev[cc], next[cc]);
+        emit(std::integral_constant<int, 2 * w>{}, mid);
+        emit(std::integral_constant<int, 2 * w + 1>{}, next);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
+      });
+    } else {
+      // UV = 4: windows yb/4, yb/4 + 1; UV = 8: rows o = 1..8 of window yb/8
+      constexpr int NWIN = G::UV == 4 ? 2 : 1;
+      static_for<NWIN>([&](auto w_c) {
+        constexpr int w = decltype(w_c)::value;
+        const int k = yb / G::UV + w;
+        s2 next[4];
+        anchor_row<W, H>(red, k, x0, next);
+        uint32_t delta[4], num[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+          delta[cc] = as_u32(next[cc]) - as_u32(prev[cc]);
+          num[cc] = as_u32(pk_mad_cc<G::UV, G::UV / 2>(as_u2(prev[cc])));
+        }
+        static_for<G::UV>([&](auto r_c) {
+          constexpr int r = decltype(r_c)::value, o = r + 1;
+          s2 prow[4];
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            if constexpr (o == G::UV) {
+              prow[cc] = next[cc];
+            } else {
+              num[cc] += delta[cc];
+              prow[cc] = as_s2(as_u2(num[cc]) >> (u2){G::LV, G::LV});
+            }
+          }
+          emit(std::integral_constant<int, w * G::UV + r>{}, prow);
+        });
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
+      });
+    }
+    acc.t0 = pair_finish(t0, acc.t0);
+    acc.t1 = pair_finish(t1, acc.t1);
+  }
+}
+
 struct Ctx {
   const SearchArgs *a;
   const uint16_t *org;        // quadrant tile of original samples
@@ -785,15 +958,29 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   wave_lds_sync();
 
   uint32_t best = 0xffffffffu;  // DEC (decisions only): argmin over the task's pairs, cost << 5 | mode
+  constexpr bool PAIRED = MIP_PAIR_BLOCKS && kPaired<W, H, V>;
 #pragma unroll 1
   for (int q = task.q0; q < task.q1; q++) {
-    std::conditional_t<(W * H <= 32), PackedAcc, Acc> acc;
+    std::conditional_t<PAIRED, PairAcc, std::conditional_t<(W * H <= 32), PackedAcc, Acc>> acc;
     s2 prev[4];
 #pragma unroll
     for (int cc = 0; cc < 4; cc++) prev[cc] = top[cc];
     phase_a<W, H, V>(x, lane, ncu, q, 0);
     wave_lds_sync();
-    if constexpr (G::CHUNKED) {
+    if constexpr (PAIRED && G::CHUNKED) {
+      walk_pairs<W, H, V>(orig, red, x0, 0, prev, acc);
+      wave_lds_sync();
+      phase_a<W, H, V>(x, lane, ncu, q, 1);
+      wave_lds_sync();
+      const Red<G::R, G::RP> red_hi{mine, -4};  // chunk 1 holds reduced rows 4..7
+      walk_pairs<W, H, V>(orig, red_hi, x0, 4, prev, acc);  // prev carries anchor row 3
+    } else if constexpr (PAIRED) {
+      const int k0 = G::V > 1 ? v * G::KV : 0;
+      if constexpr (G::V > 1) {
+        if (k0 > 0) anchor_row<W, H>(red, k0 - 1, x0, prev);
+      }
+      walk_pairs<W, H, V>(orig, red, x0, k0, prev, acc);
+    } else if constexpr (G::CHUNKED) {
       walk_strip<W, H, V>(c, rt, orig, red, x0, 0, 4, prev, acc);
       wave_lds_sync();
       phase_a<W, H, V>(x, lane, ncu, q, 1);
@@ -815,7 +1002,14 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
     constexpr int GS = G::S * G::V;
     uint32_t sad0, sad1, satd0, satd1;
     int c0, c1;  // min(2 * SAD, SATD) of the pair's modes (intra.cl:1166)
-    if constexpr (W * H <= 32) {
+    if constexpr (PAIRED) {
+      sad0 = group_sum<GS>(acc.sad0);
+      sad1 = group_sum<GS>(acc.sad1);
+      satd0 = group_sum<GS>(acc.t0) >> 1;
+      satd1 = group_sum<GS>(acc.t1) >> 1;
+      c0 = min(2 * (int)sad0, (int)satd0);
+      c1 = min(2 * (int)sad1, (int)satd1);
+    } else if constexpr (W * H <= 32) {
       const uint32_t sp = group_sum<GS>(acc.sad), tp = group_sum<GS>(acc.satd);
       const uint32_t cp = as_u32(__builtin_elementwise_min(as_u2(sp) << (u2){1, 1}, as_u2(tp)));
       c0 = (int)(cp & 0xffff);
