@@ -101,7 +101,11 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
  * best_mode_out / best_cost_out: optional per-CU decision lists, [nframes][nCTUs*5380][K]
  * with K = opts.best_k (K = 1: the argmin; mip_topk_device gives the ordering rules;
  * 0xff / MIP_COST_UNAVAILABLE for unavailable CUs).
- * sad_out / satd_out: optional (need opts.want_sad_satd).  Synchronous. */
+ * sad_out / satd_out: optional (need opts.want_sad_satd).  Synchronous.
+ * Host buffers: page-locked memory (mip_host_alloc, hipHostRegister) is transferred by DMA
+ * directly; pageable memory (malloc, the reference's return_minSadHad, main.cpp:656-668)
+ * goes through the engine's page-locked bounce ring (8 pieces of up to 64 MB, parallel host
+ * copies), allocated at its first use. */
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
                       int nframes, int32_t *costs_out, uint8_t *best_mode_out,
                       int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out);
@@ -117,7 +121,8 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
                             uint64_t *ticket);
 
 /* Block until the call with this ticket (and every earlier one) has completed: its outputs
- * are in host memory. */
+ * are in host memory.  Pageable output buffers are written (copied out of the bounce ring)
+ * by this call -- an asynchronous call with pageable outputs must be waited for. */
 int mip_wait(mip_engine *e, uint64_t ticket);
 
 /* Device-resident variant (inputs already in HBM; all pointers are device pointers,

@@ -369,6 +369,31 @@ def test_async_host_calls_in_flight(gpu_available):
     assert np.array_equal(o4["cost"][0], O.search(frames[8]))
 
 
+def test_pageable_and_pinned_host_buffers_agree(gpu_available):
+    """mip_search_frames with pageable (numpy) buffers -- staged through the engine's
+    page-locked bounce ring -- and with page-locked buffers give identical outputs; several
+    asynchronous calls with pageable outputs are in flight at once (ring pieces recycled
+    across calls, copied out by wait)."""
+    from mipgpu import pinned_empty
+    w, h, n = 392, 264, 21
+    frames = synth_frames(w, h, n, 0x9A6, 0)
+    with MipEngine(w, h, max_batch=16, want_sad_satd=True) as eng:
+        pf = pinned_empty(frames.shape, np.uint16)
+        pf[:] = frames
+        out = {k: pinned_empty((n, eng.costs_per_frame), np.int32) for k in ("cost", "sad", "satd")}
+        out.update(best_mode=pinned_empty((n, eng.cus_per_frame), np.uint8),
+                   best_cost=pinned_empty((n, eng.cus_per_frame), np.int32))
+        pinned = eng.search(pf, best=True, sad_satd=True, out=out)
+        paged = eng.search(frames, best=True, sad_satd=True)
+        tickets = [eng.search_async(frames[i:i + 7], best=True) for i in range(0, n, 7)]
+        parts = [eng.wait(t) for t in tickets]
+    for k in ("cost", "sad", "satd", "best_mode", "best_cost"):
+        assert np.array_equal(pinned[k], paged[k]), k
+    assert np.array_equal(np.concatenate([p["cost"] for p in parts]), pinned["cost"])
+    assert np.array_equal(np.concatenate([p["best_mode"] for p in parts]), pinned["best_mode"])
+    assert np.array_equal(pinned["cost"][3], O.search(frames[3]))
+
+
 def test_dropped_ticket_waits(gpu_available):
     """A search_async ticket dropped without wait(): its finaliser waits, so the output and
     input arrays it keeps alive are not freed while the engine's copies use them; the

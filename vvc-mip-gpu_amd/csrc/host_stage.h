@@ -1,0 +1,227 @@
+// host_stage.h -- page-locked bounce ring for pageable (malloc'd) host buffers of the host
+// pipeline (mip_search_frames[_async]).
+//
+// DMA from / to pageable memory is staged by the HIP runtime at ~8 GB/s (measured on MI355X,
+// profiles/r03_pageable_probe.txt); a copy engine moves ~57 GB/s from page-locked memory and
+// eight host threads copy page-locked -> pageable at ~117 GB/s.  So pageable transfers go
+// through a ring of page-locked pieces:
+//   upload    host memcpy (parallel) pageable -> piece, then the piece's DMA on the upload
+//             stream; the piece is free again once that DMA has completed;
+//   download  the piece's DMA on the download stream, then -- when a later operation needs
+//             the piece, or the call is waited for -- host memcpy (parallel) piece -> pageable.
+// Pieces are used round robin, in the order they were enqueued, so the oldest piece in flight
+// is always the next one to reuse; `complete_front` finishes it (waits for its DMA, copies a
+// download out).  The DMAs stay on the pipeline's streams, so the per-slot events that order
+// the device buffers are unchanged: a device buffer is free once the DMA has run, whether or
+// not the host copy-out has.  Not thread safe (the engine is used by one host thread at a
+// time).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace mipgpu {
+
+// Fixed pool of host threads for large memcpys (one job at a time, split evenly).
+class CopyPool {
+ public:
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; i++) th_.emplace_back([this, i] { run(i); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  // memcpy(dst, src, n) over all threads; returns when done.
+  void copy(void *dst, const void *src, size_t n) {
+    if (n < (4u << 20) || th_.empty()) {
+      memcpy(dst, src, n);
+      return;
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    dst_ = (char *)dst;
+    src_ = (const char *)src;
+    n_ = n;
+    pending_ = (int)th_.size();
+    gen_++;
+    cv_.notify_all();
+    done_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void run(int i) {
+    unsigned seen = 0;
+    for (;;) {
+      char *d;
+      const char *s;
+      size_t n;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        d = dst_, s = src_, n = n_;
+      }
+      const size_t nt = th_.size(), per = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
+      const size_t o = (size_t)i * per;
+      if (o < n) memcpy(d + o, s + o, std::min(per, n - o));
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--pending_ == 0) done_.notify_all();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  bool stop_ = false;
+  unsigned gen_ = 0;
+  int pending_ = 0;
+  char *dst_ = nullptr;
+  const char *src_ = nullptr;
+  size_t n_ = 0;
+};
+
+class HostStage {
+ public:
+  static constexpr int kRing = 8;
+
+  ~HostStage() { release(); }
+
+  // Page-locked host memory (mip_host_alloc / hipHostRegister) or device memory: transfers
+  // run at DMA rate without staging.
+  static bool pinned(const void *p) {
+    hipPointerAttribute_t at{};
+    const hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // unregistered host memory reports an error: clear it
+      return false;
+    }
+    return at.type == hipMemoryTypeHost || at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+  }
+
+  // Allocate the ring (pieces of `piece` bytes) if it is not there or smaller.
+  hipError_t reserve(size_t piece) {
+    piece = std::max<size_t>(piece, 1u << 20);
+    if (piece_ >= piece) return hipSuccess;
+    hipError_t e = drain(~0ull);
+    if (e != hipSuccess) return e;
+    release();
+    for (int i = 0; i < kRing; i++) {
+      if ((e = hipHostMalloc((void **)&buf_[i], piece, hipHostMallocDefault)) != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    piece_ = piece;
+    if (!pool_) pool_.reset(new CopyPool(8));
+    return hipSuccess;
+  }
+
+  size_t piece() const { return piece_; }
+
+  // Pageable host -> device on stream s (the source is copied before this returns).
+  hipError_t upload(void *dst_dev, const void *src, size_t n, hipStream_t s, uint64_t call) {
+    for (size_t o = 0; o < n; o += piece_) {
+      const size_t len = std::min(piece_, n - o);
+      int j;
+      hipError_t e = take(&j);
+      if (e != hipSuccess) return e;
+      pool_->copy(buf_[j], (const char *)src + o, len);
+      if ((e = hipMemcpyAsync((char *)dst_dev + o, buf_[j], len, hipMemcpyHostToDevice, s)) != hipSuccess ||
+          (e = hipEventRecord(ev_[j], s)) != hipSuccess)
+        return e;
+      fifo_.push_back({j, nullptr, len, call});
+    }
+    return hipSuccess;
+  }
+
+  // Device -> pageable host on stream s; the host side is written by complete_front / drain.
+  hipError_t download(void *dst, const void *src_dev, size_t n, hipStream_t s, uint64_t call) {
+    for (size_t o = 0; o < n; o += piece_) {
+      const size_t len = std::min(piece_, n - o);
+      int j;
+      hipError_t e = take(&j);
+      if (e != hipSuccess) return e;
+      if ((e = hipMemcpyAsync(buf_[j], (const char *)src_dev + o, len, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+          (e = hipEventRecord(ev_[j], s)) != hipSuccess)
+        return e;
+      fifo_.push_back({j, (char *)dst + o, len, call});
+    }
+    return hipSuccess;
+  }
+
+  // Finish every piece of calls <= `call` (and the pieces enqueued before them).
+  hipError_t drain(uint64_t call) {
+    while (!fifo_.empty() && fifo_.front().call <= call) {
+      const hipError_t e = complete_front();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+
+  bool idle() const { return fifo_.empty(); }
+
+  // Drop every piece after its DMA has finished, without copying downloads out (engine
+  // teardown: the caller's buffers of calls never waited for may be gone).
+  void abandon() {
+    for (const Piece &p : fifo_) (void)hipEventSynchronize(ev_[p.ring]);
+    fifo_.clear();
+  }
+
+ private:
+  struct Piece {
+    int ring;
+    char *dst;  // download: pageable destination; upload: nullptr
+    size_t bytes;
+    uint64_t call;
+  };
+
+  hipError_t complete_front() {
+    const Piece p = fifo_.front();
+    const hipError_t e = hipEventSynchronize(ev_[p.ring]);
+    if (e != hipSuccess) return e;
+    if (p.dst) pool_->copy(p.dst, buf_[p.ring], p.bytes);
+    fifo_.pop_front();
+    return hipSuccess;
+  }
+
+  hipError_t take(int *j) {
+    if ((int)fifo_.size() == kRing) {
+      const hipError_t e = complete_front();
+      if (e != hipSuccess) return e;
+    }
+    *j = next_;
+    next_ = (next_ + 1) % kRing;
+    return hipSuccess;
+  }
+
+  void release() {
+    for (int i = 0; i < kRing; i++) {
+      if (buf_[i]) (void)hipHostFree(buf_[i]);
+      if (ev_[i]) (void)hipEventDestroy(ev_[i]);
+      buf_[i] = nullptr;
+      ev_[i] = nullptr;
+    }
+    piece_ = 0;
+    next_ = 0;
+  }
+
+  char *buf_[kRing] = {};
+  hipEvent_t ev_[kRing] = {};
+  size_t piece_ = 0;
+  int next_ = 0;
+  std::deque<Piece> fifo_;
+  std::unique_ptr<CopyPool> pool_;
+};
+
+}  // namespace mipgpu

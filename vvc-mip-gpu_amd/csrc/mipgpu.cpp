@@ -16,6 +16,7 @@
 
 #include "mip_kernels.h"
 #include "mip_tables.h"
+#include "host_stage.h"
 #include "queue_ring.h"
 
 namespace {
@@ -361,6 +362,8 @@ struct mip_engine {
   uint64_t tr_chunk[kHostSlots] = {};
   int tr_frames[kHostSlots] = {}, tr_filter[kHostSlots] = {};
   std::vector<std::pair<double, double>> tr_times;
+  // Page-locked bounce ring for pageable caller buffers of the host pipeline (host_stage.h).
+  mipgpu::HostStage stage;
   uint16_t *d_frames = nullptr, *d_refs = nullptr;
   int32_t *d_costs = nullptr, *d_sad = nullptr, *d_satd = nullptr, *d_best_cost = nullptr;
   uint8_t *d_best = nullptr;
@@ -479,6 +482,7 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   if (e->stream3) (void)hipStreamSynchronize(e->stream3);
+  e->stage.abandon();
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables,
                   (void *)e->d_ctu_var[0], (void *)e->d_ctu_var[1], (void *)e->d_fixup})
@@ -777,7 +781,7 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
 
 static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                                 int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
-                                int32_t *satd_out);
+                                int32_t *satd_out, uint64_t call);
 
 // mip_trace_times: read the pending chunk times of slot `sl` (waits for its events).
 static int drain_trace(mip_engine *e, int sl) {
@@ -803,7 +807,7 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
   HIP_TRY(hipSetDevice(e->device));
   const int rc = search_frames_chunks(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out,
-                                      sad_out, satd_out);
+                                      sad_out, satd_out, e->host_calls + 1);
   // Also after a failure part-way through the chunks: the chunks already queued on the
   // upload / search streams are covered by host_done (later device-API searches that filter
   // into the engine's reference scratch wait for it) and by this call's completion event.
@@ -815,6 +819,9 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
     (void)hipStreamSynchronize(e->stream2);
     (void)hipStreamSynchronize(e->stream);
     (void)hipStreamSynchronize(e->stream3);
+    // staged downloads of the calls before this one complete normally; this call's are dropped
+    (void)e->stage.drain(e->host_calls);
+    e->stage.abandon();
     g_err = err;
     return rc;
   }
@@ -829,7 +836,7 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
 
 static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                                 int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
-                                int32_t *satd_out) {
+                                int32_t *satd_out, uint64_t call) {
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
     HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
@@ -845,11 +852,29 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // of the slot's outputs, the download waits for the search.  The chunk sequence (and so
   // the slot rotation and these waits) continues across calls, so asynchronous calls queue
   // behind each other without draining the pipeline.  Transfers run at DMA rate from
-  // page-locked host memory (mip_host_alloc); pageable buffers are staged by the runtime.
+  // page-locked host memory (mip_host_alloc); pageable buffers go through the engine's
+  // page-locked bounce ring (host_stage.h), their downloads finished by mip_wait.
   const int nslots = e->opts.max_batch >= 16 ? 4 : (e->opts.max_batch >= 2 ? 2 : 1);
   const int sb = e->opts.max_batch / nslots;
   const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
   const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
+  const bool pin_in = mipgpu::HostStage::pinned(frames) && (!refs_or_null || mipgpu::HostStage::pinned(refs_or_null));
+  const bool pin_cost = !costs_out || mipgpu::HostStage::pinned(costs_out);
+  const bool pin_sad = !sad_out || mipgpu::HostStage::pinned(sad_out);
+  const bool pin_satd = !satd_out || mipgpu::HostStage::pinned(satd_out);
+  const bool pin_bm = !best_mode_out || mipgpu::HostStage::pinned(best_mode_out);
+  const bool pin_bc = !best_cost_out || mipgpu::HostStage::pinned(best_cost_out);
+  if (!(pin_in && pin_cost && pin_sad && pin_satd && pin_bm && pin_bc)) {
+    const size_t most = std::max({(size_t)sb * fs * 2, (size_t)sb * cpf * 4, (size_t)sb * upf * 4});
+    HIP_TRY(e->stage.reserve(std::min<size_t>(most, 64u << 20)));
+  }
+  // host <-> device copy on stream s: DMA from / to page-locked memory, else the bounce ring
+  auto to_dev = [&](void *d, const void *h, size_t n, bool pinned) {
+    return pinned ? hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, up) : e->stage.upload(d, h, n, up, call);
+  };
+  auto to_host = [&](void *h, const void *d, size_t n, bool pinned) {
+    return pinned ? hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, down) : e->stage.download(h, d, n, down, call);
+  };
   for (int f0 = 0; f0 < nframes; f0 += sb) {
     const int nb = std::min(sb, nframes - f0);
     const uint64_t k = e->host_chunks++;
@@ -862,11 +887,11 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
       if (drain_trace(e, sl) != 0) return -1;
       HIP_TRY(hipEventRecord(e->tr_ev[sl][0], up));
     }
-    HIP_TRY(hipMemcpyAsync(d_frames, frames + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, up));
+    HIP_TRY(to_dev(d_frames, frames + f0 * fs, nb * fs * 2, pin_in));
     if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][1], up));
     const uint16_t *d_refs = nullptr;
     if (refs_or_null) {
-      HIP_TRY(hipMemcpyAsync(e->d_refs + fo * fs, refs_or_null + f0 * fs, nb * fs * 2, hipMemcpyHostToDevice, up));
+      HIP_TRY(to_dev(e->d_refs + fo * fs, refs_or_null + f0 * fs, nb * fs * 2, pin_in));
       d_refs = e->d_refs + fo * fs;
     }
     HIP_TRY(hipEventRecord(e->slot_up[sl], up));
@@ -898,12 +923,11 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     if (!any_out) continue;
     HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));
-    if (costs_out) HIP_TRY(hipMemcpyAsync(costs_out + f0 * cpf, d_costs, nb * cpf * 4, hipMemcpyDeviceToHost, down));
-    if (sad_out) HIP_TRY(hipMemcpyAsync(sad_out + f0 * cpf, d_sad, nb * cpf * 4, hipMemcpyDeviceToHost, down));
-    if (satd_out) HIP_TRY(hipMemcpyAsync(satd_out + f0 * cpf, d_satd, nb * cpf * 4, hipMemcpyDeviceToHost, down));
-    if (best_mode_out) HIP_TRY(hipMemcpyAsync(best_mode_out + f0 * upf, d_best, nb * upf, hipMemcpyDeviceToHost, down));
-    if (best_cost_out)
-      HIP_TRY(hipMemcpyAsync(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, hipMemcpyDeviceToHost, down));
+    if (costs_out) HIP_TRY(to_host(costs_out + f0 * cpf, d_costs, nb * cpf * 4, pin_cost));
+    if (sad_out) HIP_TRY(to_host(sad_out + f0 * cpf, d_sad, nb * cpf * 4, pin_sad));
+    if (satd_out) HIP_TRY(to_host(satd_out + f0 * cpf, d_satd, nb * cpf * 4, pin_satd));
+    if (best_mode_out) HIP_TRY(to_host(best_mode_out + f0 * upf, d_best, nb * upf, pin_bm));
+    if (best_cost_out) HIP_TRY(to_host(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, pin_bc));
     HIP_TRY(hipEventRecord(e->slot_down[sl], down));
   }
   return 0;
@@ -916,6 +940,8 @@ int mip_wait(mip_engine *e, uint64_t ticket) {
   // a ticket older than the ring shares its event with a later call: waiting for that one
   // is later than needed, never too early
   HIP_TRY(hipEventSynchronize(e->call_done[(ticket - 1) % mip_engine::kCallRing]));
+  // pageable outputs: copy the call's staged downloads out (and everything queued before)
+  HIP_TRY(e->stage.drain(ticket));
   return 0;
 }
 
