@@ -435,12 +435,14 @@ def test_async_host_calls_and_device_filter_scratch(gpu_available):
                                         (392, 264, "filterFrame_2d_float_5x5_quarterCtu", 2),
                                         (416, 240, "filterFrame_1d_int_5x5", 2)])
 def test_device_decisions_only_fused_argmin(gpu_available, w, h, filt, k):
-    """mip_search_device without a cost table (costs=False): the search keeps each CU's
-    argmin (cost << 5 | mode, atomicMin per task -- tasks that cut a CU's mode pairs meet in
-    one entry) and unpacks it; must equal the argmin of the oracle's table (ties to the lower
-    mode, unavailable CUs 0xff / MIP_COST_UNAVAILABLE), for 1..3-frame batches (different
-    task cuts per slice count).  416x240 with a separable filter: reference samples above 10
-    bits in the last columns (the exact per-CU kernel's CUs write their argmin directly)."""
+    """mip_search_device without a cost table (costs=False): a task with all of a CU's mode
+    pairs writes the CU's decision directly; tasks that cut a CU's pairs meet in a packed
+    argmin (cost << 5 | mode, atomicMin) unpacked after the launch; undefined CUs are written
+    from the decisions-only fill lists.  Must equal the argmin of the oracle's table (ties to
+    the lower mode, unavailable CUs 0xff / MIP_COST_UNAVAILABLE) on every entry (outputs start
+    as a sentinel: an entry nobody writes fails), for 1..3-frame batches (different task cuts
+    per slice count).  416x240 with a separable filter: reference samples above 10 bits in the
+    last columns (the exact per-CU kernel's CUs write their decision directly)."""
     import torch
     n = 3
     frames = synth_frames(w, h, n, 0xD0 + w, 1)
@@ -454,8 +456,8 @@ def test_device_decisions_only_fused_argmin(gpu_available, w, h, filt, k):
     d = torch.from_numpy(frames.astype(np.int16)).cuda()
     with MipEngine(w, h, max_batch=n, filter=filt, kernel_idx=k) as eng:
         for nb in (1, 2, 3):
-            bm = torch.empty((nb, eng.cus_per_frame), dtype=torch.uint8, device="cuda")
-            bc = torch.empty((nb, eng.cus_per_frame), dtype=torch.int32, device="cuda")
+            bm = torch.full((nb, eng.cus_per_frame), 0x5a, dtype=torch.uint8, device="cuda")
+            bc = torch.full((nb, eng.cus_per_frame), -5, dtype=torch.int32, device="cuda")
             assert eng.search_device(d[:nb], costs=False, best_mode=bm, best_cost=bc) is None
             torch.cuda.synchronize()
             for f in range(nb):
@@ -495,8 +497,8 @@ def test_prefetching_launch_equals_small_launches(gpu_available):
         small = torch.empty_like(big)
         for f in range(0, n, 2):
             eng.search_device(frames[f:f + 2], costs=small[f:f + 2])
-        bm = torch.empty((n, eng.cus_per_frame), dtype=torch.uint8, device="cuda")
-        bc = torch.empty((n, eng.cus_per_frame), dtype=torch.int32, device="cuda")
+        bm = torch.full((n, eng.cus_per_frame), 0x5a, dtype=torch.uint8, device="cuda")
+        bc = torch.full((n, eng.cus_per_frame), -5, dtype=torch.int32, device="cuda")
         eng.search_device(frames, costs=False, best_mode=bm, best_cost=bc)
         tm, tc = topk_device(big, W, H, 1)
         torch.cuda.synchronize()

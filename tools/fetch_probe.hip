@@ -5,7 +5,11 @@
 //   read16   16-byte loads per lane (the filter's staging; the MI355X guide's x2 case)
 //   window8  the search kernel's quadrant windows: rows of 68 samples starting 4 samples
 //            before each 64-sample quadrant, 65 rows, 8-byte chunks (tile_load's pattern)
-// FETCH_SIZE (KiB) x 1024 / bytes read = the correction factor for that load width.
+//   write8   8-byte stores per lane, coalesced (1 GiB)
+//   wstride  the search kernel's cost stores: lane = CU with a 128-byte row of 32 int32
+//            costs, each store instruction writes 8 bytes (one mode pair) of 64 rows, 16
+//            instructions fill the rows (1 GiB)
+// FETCH_SIZE / WRITE_SIZE (KiB) x 1024 / bytes = the correction factor for that access.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -22,6 +26,16 @@ __global__ void read16(const uint4 *in, size_t n, unsigned *out) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     acc += in[i].x ^ in[i].y ^ in[i].z ^ in[i].w;
   if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
+__global__ void write8(uint2 *o, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    o[i] = make_uint2((unsigned)i, 1u);
+}
+
+__global__ void wstride(uint2 *o, size_t rows) {  // rows of 16 uint2
+  for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < rows; r += (size_t)gridDim.x * blockDim.x)
+    for (int p = 0; p < 16; p++) o[r * 16 + p] = make_uint2((unsigned)r, (unsigned)p);
 }
 
 // frame W x H of uint16 (W multiple of 128); one workgroup per 64x64 quadrant
@@ -50,6 +64,8 @@ int main() {
   read16<<<4096, 256>>>((const uint4 *)buf, bytes / 16, out);
   const int W = 7680, H = (int)(bytes / 2 / 7680) / 64 * 64;  // 1 GiB of 8K-wide rows
   window8<<<(W / 64) * (H / 64), 256>>>((const uint16_t *)buf, W, H, out);
+  write8<<<4096, 256>>>((uint2 *)buf, bytes / 8);
+  wstride<<<4096, 256>>>((uint2 *)buf, bytes / 128);
   hipDeviceSynchronize();
   printf("bytes per kernel: read8 %zu, read16 %zu, window8 unique %zu (rows read %zu)\n", bytes, bytes,
          (size_t)W * H * 2, (size_t)(W / 64) * (H / 64) * 65 * 136);

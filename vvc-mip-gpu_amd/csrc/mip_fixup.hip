@@ -174,7 +174,11 @@ __global__ __launch_bounds__(64) void fixup_kernel(SearchArgs a, const FixupCu *
     }
     __syncthreads();  // rpred / pred are rewritten by the next mode
   }
-  if (!a.cost && t == 0) a.best[((size_t)frame * a.nctus + c.ctu) * MIP_CUS_PER_CTU + c.cu] = best;
+  if (!a.cost && t == 0) {  // decisions only: fixup CUs are never split
+    const size_t g = ((size_t)frame * a.nctus + c.ctu) * MIP_CUS_PER_CTU + c.cu;
+    if (a.best_mode) a.best_mode[g] = (uint8_t)(best & 31);
+    a.best_cost[g] = (int32_t)(best >> 5);
+  }
 }
 
 }  // namespace
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(64) void fixup_kernel(SearchArgs a, const FixupCu *
 hipError_t launch_fixup(const SearchArgs &a, const FixupCu *cus, int n, int nframes, hipStream_t s) {
   if (n < 1 || nframes < 1) return hipSuccess;
   const long long groups = (long long)n * nframes;
-  if (groups >= (1LL << 31) || !cus || (!a.cost && !a.best)) return hipErrorInvalidValue;
+  if (groups >= (1LL << 31) || !cus || (!a.cost && !a.best_cost)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fixup_kernel, dim3((unsigned)groups), dim3(64), 0, s, a, cus, n);
   return hipGetLastError();
 }

@@ -49,8 +49,16 @@ struct SearchArgs {
   const uint16_t *orig;   // [frames][height][width] original samples (distortion)
   const uint16_t *refs;   // reference-sample source: == orig, or the filtered frames
   int32_t *cost;          // [frames][nctus][97840]  min(2*SAD, SATD); null: decisions only
-  uint32_t *best;         // optional: [frames][nctus][5380] running argmin (cost << 5 | mode),
-                          // all ones at launch (atomicMin per task and CU)
+  // Decisions only ([frames][nctus][5380] per-CU best mode / cost): a task that searches
+  // all of a CU's mode pairs writes the CU's decision directly; CUs whose pairs are cut over
+  // several tasks (the `split` lists) meet in best_cost as a packed running argmin
+  // (cost << 5 | mode, all ones before the launch, atomicMin), unpacked after it
+  // (launch_dec_split); CUs the reference leaves undefined get 0xff / kUnavailable from the
+  // `dfill` lists.
+  uint8_t *best_mode;     // optional
+  int32_t *best_cost;
+  const uint16_t *dfill;  // undefined CUs of (v, q): CU indices inside the CTU,
+  const int *dfill_begin; // [dfill_begin[4v+q], dfill_begin[4v+q+1])
   int32_t *sad;           // optional, same layout
   int32_t *satd;          // optional, same layout
   const WaveTask *tasks;  // per (quadrant, wave) task lists, concatenated
@@ -129,12 +137,22 @@ int search_waves_per_group();
 int search_resident_groups(bool alt_refs);
 hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, hipStream_t s);
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
-// packed argmin (SearchArgs::best) -> per-CU best mode / cost (k = 1 decision lists)
-hipError_t launch_unpack_best(const uint32_t *packed, uint8_t *best_mode, int32_t *best_cost, int total_cus,
-                              hipStream_t s);
+// Decisions only, CUs whose mode pairs are cut over several tasks (split CUs of the CTU's
+// variant: [split_begin[v], split_begin[v+1]) of `split`, at most max_split per variant):
+// init = true sets their best_cost entries to all ones (before the search); init = false
+// unpacks the packed argmin in place into best_mode / best_cost (after it).
+struct SplitArgs {
+  const uint16_t *split;
+  const int *split_begin;
+  const uint8_t *ctu_var;
+  uint8_t *best_mode;
+  int32_t *best_cost;
+  int nctus, ctu0, nrange, max_split;
+};
+hipError_t launch_dec_split(const SplitArgs &a, int nframes, bool init, hipStream_t s);
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s);
 // Exact per-CU search of `n` CUs of every frame (same outputs as the search kernel: cost /
-// SAD / SATD tables or, decisions only, the packed argmin in a.best).
+// SAD / SATD tables or, decisions only, the decision in a.best_mode / a.best_cost).
 hipError_t launch_fixup(const SearchArgs &a, const FixupCu *cus, int n, int nframes, hipStream_t s);
 
 }  // namespace mipgpu

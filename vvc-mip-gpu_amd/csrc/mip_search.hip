@@ -1036,9 +1036,18 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       }
     }
   }
-  // tasks that cut a CU's mode pairs meet in one entry: atomicMin of the packed argmins
-  if (DEC && active && sub == G::S * G::V - 1)
-    atomicMin(a.best + ((size_t)x.frame * a.nctus + x.ctu) * MIP_CUS_PER_CTU + job.cu, best);
+  // decisions only: a task with all of a CU's pairs writes its decision; tasks that cut a
+  // CU's pairs meet in one entry (atomicMin of the packed argmins, unpacked after the launch)
+  if (DEC && active && sub == G::S * G::V - 1) {
+    constexpr int kPairs = G::SID == 2 ? 6 : (G::SID == 1 ? 8 : 16);
+    const size_t g = ((size_t)x.frame * a.nctus + x.ctu) * MIP_CUS_PER_CTU + job.cu;
+    if (task.q0 == 0 && task.q1 == kPairs) {
+      if (a.best_mode) a.best_mode[g] = (uint8_t)(best & 31);
+      a.best_cost[g] = (int32_t)(best >> 5);
+    } else {
+      atomicMin(reinterpret_cast<uint32_t *>(a.best_cost) + g, best);
+    }
+  }
 }
 
 // Stage the quadrant window (rows -1..63, columns -4..63) of one frame into LDS, each
@@ -1152,7 +1161,7 @@ constexpr int kOrgTiles = PF && !ALT ? 2 : 1;
 constexpr int kCounterWords = 8;  // [parity]: next task, finished waves, item, item taken late
 constexpr uint32_t kTakeItem = 0xffffffffu;  // "take the next item after this one" (PF)
 
-// DEC: decisions only -- no cost table, a per-CU packed argmin (SearchArgs::best).
+// DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
 template <bool ALT, bool DEC, bool PF_>
 __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = PF_ && !ALT;
@@ -1199,8 +1208,15 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     uint16_t *ref = ALT ? lattice : org;
 
     // CUs whose cost the reference leaves undefined (edge CTUs): MIP_COST_UNAVAILABLE, no search
-    // (decisions only: their entries keep the launch's all-ones = unavailable)
-    if (!DEC) {
+    if (DEC) {
+      const size_t gbase = ((size_t)frame * a.nctus + ctu) * MIP_CUS_PER_CTU;
+      const int f0 = a.dfill_begin[vq], nf = a.dfill_begin[vq + 1] - f0;
+      for (int i = slice * blockDim.x + threadIdx.x; i < nf; i += a.slices * blockDim.x) {
+        const size_t g = gbase + a.dfill[f0 + i];
+        if (a.best_mode) a.best_mode[g] = 0xff;
+        a.best_cost[g] = kUnavailable;
+      }
+    } else {
       const size_t cbase = ((size_t)frame * a.nctus + ctu) * (MIP_COSTS_PER_CTU / 4);
       const int f0 = a.fill_begin[vq], nf = a.fill_begin[vq + 1] - f0;
       const uint4 un = make_uint4(kUnavailable, kUnavailable, kUnavailable, kUnavailable);
@@ -1360,15 +1376,24 @@ __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
   }
 }
 
-// Packed argmin -> decision list of length 1 (the layout of best_mode_kernel with k = 1).
-__global__ __launch_bounds__(256) void unpack_best_kernel(const uint32_t *packed, uint8_t *best_mode, int32_t *best_cost,
-                                                          int total) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= total) return;
-  const uint32_t p = packed[g];
-  const bool ok = p != 0xffffffffu;
-  if (best_mode) best_mode[g] = ok ? (uint8_t)(p & 31) : (uint8_t)0xff;
-  if (best_cost) best_cost[g] = ok ? (int32_t)(p >> 5) : kUnavailable;
+// Split CUs of decisions-only searches: all ones before the search (init), packed argmin ->
+// decision list of length 1 after it (the layout of best_mode_kernel with k = 1).
+template <bool INIT>
+__global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int j = t % a.max_split, r = t / a.max_split, ctu = a.ctu0 + r % a.nrange, frame = r / a.nrange;
+  const int v = a.ctu_var[ctu], b = a.split_begin[v];
+  if (j >= a.split_begin[v + 1] - b) return;
+  const size_t g = ((size_t)frame * a.nctus + ctu) * MIP_CUS_PER_CTU + a.split[b + j];
+  if (INIT) {
+    a.best_cost[g] = -1;
+  } else {
+    const uint32_t p = (uint32_t)a.best_cost[g];
+    const bool ok = p != 0xffffffffu;
+    if (a.best_mode) a.best_mode[g] = ok ? (uint8_t)(p & 31) : (uint8_t)0xff;
+    a.best_cost[g] = ok ? (int32_t)(p >> 5) : kUnavailable;
+  }
 }
 
 }  // namespace
@@ -1408,7 +1433,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;
-  if (dec && !a.best) return hipErrorInvalidValue;
+  if (dec && (!a.best_cost || !a.dfill_begin)) return hipErrorInvalidValue;
   const bool pf = !alt_refs && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
   const size_t lds = search_lds_bytes(alt_refs, pf);
   const dim3 grid(groups), block(64 * kWaves);
@@ -1425,11 +1450,13 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   return hipGetLastError();
 }
 
-hipError_t launch_unpack_best(const uint32_t *packed, uint8_t *best_mode, int32_t *best_cost, int total_cus,
-                              hipStream_t s) {
-  if (!packed || total_cus < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(unpack_best_kernel, dim3((total_cus + 255) / 256), dim3(256), 0, s, packed, best_mode, best_cost,
-                     total_cus);
+hipError_t launch_dec_split(const SplitArgs &a, int nframes, bool init, hipStream_t s) {
+  if (a.max_split < 1) return hipSuccess;  // no split CUs
+  const long long total = (long long)nframes * a.nrange * a.max_split;
+  if (!a.best_cost || !a.split || total >= (1LL << 31)) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (init) hipLaunchKernelGGL(dec_split_kernel<true>, grid, dim3(256), 0, s, a, (int)total);
+  else hipLaunchKernelGGL(dec_split_kernel<false>, grid, dim3(256), 0, s, a, (int)total);
   return hipGetLastError();
 }
 

@@ -119,6 +119,11 @@ struct WorkLists {
   std::vector<int> list_begin;   // [variant][quadrant][slice] + 1
   std::vector<uint32_t> fill;    // unavailable cost entries, uint4 index inside the CTU block
   std::vector<int> fill_begin;   // [variant][quadrant] + 1
+  // decisions only: undefined CUs (CU index inside the CTU) per [variant][quadrant], and the
+  // CUs whose mode pairs are cut over several tasks per [variant]
+  std::vector<uint16_t> dfill, split;
+  std::vector<int> dfill_begin, split_begin;
+  int max_split = 0;
 };
 
 bool shape_selected(int s) {
@@ -234,6 +239,11 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
   for (int vq = 0; vq < 4 * (int)cv.pattern.size(); vq++) {
     const int var = vq / 4, q = vq % 4;
     wl.fill_begin.push_back((int)wl.fill.size());
+    wl.dfill_begin.push_back((int)wl.dfill.size());
+    if (q == 0) {
+      if (var > 0) wl.max_split = std::max(wl.max_split, (int)wl.split.size() - wl.split_begin.back());
+      wl.split_begin.push_back((int)wl.split.size());
+    }
     struct Piece { mipgpu::WaveTask t; double cost; };
     std::vector<Piece> pieces;
     std::vector<std::vector<mipgpu::Job>> cls_cus(mipgpu::kNumClasses);
@@ -248,6 +258,7 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
         if (!cv.pattern[var][shape_cu0 + cu]) {
           const uint32_t off = sd.cost_offset + cu * 2 * sd.modes;  // multiple of 4 entries
           for (uint32_t u = 0; u < (uint32_t)(2 * sd.modes) / 4; u++) wl.fill.push_back(off / 4 + u);
+          wl.dfill.push_back((uint16_t)(shape_cu0 + cu));
           continue;
         }
         cls_cus[cls].push_back(mipgpu::Job{(uint32_t)(sd.cost_offset + cu * 2 * sd.modes), (uint8_t)(x % 64),
@@ -299,6 +310,8 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
     for (const Piece &p : pieces) {
       const int np = p.t.q1 - p.t.q0;
       const int parts = std::max(1, std::min(np, (int)std::ceil(p.cost * np / cap)));
+      if (parts > 1)
+        for (uint32_t j = 0; j < p.t.ncu; j++) wl.split.push_back(wl.jobs[p.t.cu0 + j].cu);
       for (int i = 0; i < parts; i++) {
         Piece c = p;
         c.t.q0 = (uint8_t)(p.t.q0 + np * i / parts);
@@ -324,6 +337,10 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
   }
   wl.list_begin.push_back((int)wl.tasks.size());
   wl.fill_begin.push_back((int)wl.fill.size());
+  wl.dfill_begin.push_back((int)wl.dfill.size());
+  if (!wl.split_begin.empty())
+    wl.max_split = std::max(wl.max_split, (int)wl.split.size() - wl.split_begin.back());
+  wl.split_begin.push_back((int)wl.split.size());
   return wl;
 }
 
@@ -376,6 +393,9 @@ struct mip_engine {
     int *d_lists = nullptr;
     uint32_t *d_fill = nullptr;
     int *d_fill_begin = nullptr;
+    uint16_t *d_dfill = nullptr, *d_split = nullptr;  // decisions only (WorkLists)
+    int *d_dfill_begin = nullptr, *d_split_begin = nullptr;
+    int max_split = 0;
   };
   std::vector<Work> work;
   uint8_t *d_tables = nullptr;
@@ -501,7 +521,8 @@ int mip_engine_destroy(mip_engine *e) {
     for (hipEvent_t ev : evs)
       if (ev) (void)hipEventDestroy(ev);
   for (const mip_engine::Work &w : e->work)
-    for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin})
+    for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin,
+                    (void *)w.d_dfill, (void *)w.d_dfill_begin, (void *)w.d_split, (void *)w.d_split_begin})
       if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -618,6 +639,22 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
           hipMemcpy(ew.d_jobs, wl.jobs.data(), wl.jobs.size() * sizeof(mipgpu::Job), hipMemcpyHostToDevice) != hipSuccess)) ||
         hipMemcpy(ew.d_lists, wl.list_begin.data(), wl.list_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
       return cleanup(fail("uploading work lists failed"));
+    ew.max_split = wl.max_split;
+    if (getenv("MIPGPU_WORK_STATS"))  // diagnostic: list sizes per slice count
+      fprintf(stderr, "mipgpu work %dx%d slices %d: %zu tasks, %zu jobs, %zu fill, %zu undefined CUs, %zu split CUs (max %d per CTU)\n",
+              width, height, sl, wl.tasks.size(), wl.jobs.size(), wl.fill.size(), wl.dfill.size(), wl.split.size(),
+              wl.max_split);
+    ALLOC(ew.d_dfill, std::max<size_t>(1, wl.dfill.size()) * sizeof(uint16_t));
+    ALLOC(ew.d_dfill_begin, wl.dfill_begin.size() * sizeof(int));
+    ALLOC(ew.d_split, std::max<size_t>(1, wl.split.size()) * sizeof(uint16_t));
+    ALLOC(ew.d_split_begin, wl.split_begin.size() * sizeof(int));
+    if ((!wl.dfill.empty() &&
+         hipMemcpy(ew.d_dfill, wl.dfill.data(), wl.dfill.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) ||
+        (!wl.split.empty() &&
+         hipMemcpy(ew.d_split, wl.split.data(), wl.split.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(ew.d_dfill_begin, wl.dfill_begin.data(), wl.dfill_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ew.d_split_begin, wl.split_begin.data(), wl.split_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail("uploading decision lists failed"));
   }
   const std::vector<uint8_t> tab = build_tables();
   ALLOC(e->d_tables, tab.size());
@@ -653,8 +690,9 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
                               int32_t *d_best_cost, hipStream_t s, int ctu0 = 0, int nrange = -1) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
-  // Decisions only (no cost table): the search keeps a per-CU argmin packed as
-  // (cost << 5 | mode) in d_best_cost and a small kernel unpacks it in place.
+  // Decisions only (no cost table): the search writes each CU's decision into d_best /
+  // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
+  // (cost << 5 | mode) in d_best_cost, set to all ones before and unpacked after the search.
   const bool decisions_only = d_costs == nullptr;
   if (decisions_only) {
     if (!d_best_cost) return fail("a search without d_costs needs d_best_cost (decisions only)");
@@ -682,7 +720,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.orig = d_frames;
   a.refs = alt ? refs : d_frames;
   a.cost = d_costs;
-  a.best = decisions_only ? reinterpret_cast<uint32_t *>(d_best_cost) : nullptr;
+  a.best_mode = decisions_only ? d_best : nullptr;
+  a.best_cost = decisions_only ? d_best_cost : nullptr;
   a.sad = d_sad;
   a.satd = d_satd;
   const mip_engine::Work &work = pick_work(e, nframes, nrange);
@@ -691,6 +730,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.list_begin = work.d_lists;
   a.fill = work.d_fill;
   a.fill_begin = work.d_fill_begin;
+  a.dfill = work.d_dfill;
+  a.dfill_begin = work.d_dfill_begin;
   a.tables = reinterpret_cast<const uint4 *>(e->d_tables);
   a.ctu_var = e->d_ctu_var[alt ? 1 : 0];
   a.width = e->width;
@@ -725,7 +766,9 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
       }
     }
   }
-  if (decisions_only) HIP_TRY(hipMemsetAsync(d_best_cost, 0xff, (size_t)total_cus * 4, s));
+  const mipgpu::SplitArgs sa{work.d_split, work.d_split_begin, a.ctu_var, d_best, d_best_cost,
+                             e->nctus, ctu0, nrange, work.max_split};
+  if (decisions_only) HIP_TRY(mipgpu::launch_dec_split(sa, nframes, true, s));
   const int slot = e->queue.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + 2 * slot;
@@ -750,7 +793,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     }
   }
   if (decisions_only) {
-    HIP_TRY(mipgpu::launch_unpack_best(a.best, d_best, d_best_cost, (int)total_cus, s));
+    HIP_TRY(mipgpu::launch_dec_split(sa, nframes, false, s));
   } else if (d_best || d_best_cost) {
     mipgpu::BestArgs b{d_costs, d_best, d_best_cost, (int)total_cus, e->opts.best_k};
     HIP_TRY(mipgpu::launch_best_modes(b, s));
