@@ -74,13 +74,20 @@ struct SearchArgs {
   int ctu0, nrange;       // CTUs searched: [ctu0, ctu0 + nrange) of every frame (whole frame:
                           // 0, nctus); cost entries of the other CTUs are not written
   int slices;             // workgroups (task lists) per CTU quadrant
-  uint32_t *queue;        // item counter pair {next item, workgroups done}, zero at launch;
-                          // the kernel leaves it zero again
+  uint32_t *queue;        // kQueueWords counters, zero at launch (the kernel leaves them zero
+                          // again): [c] next item of chunk c (c < kQueueChunks), then
+                          // [kQueueChunks] workgroups done
   uint32_t nitems;        // frames * nrange * 4 * slices (set by launch_search)
+  uint32_t chunks;        // queue chunks, 1..kQueueChunks (set by launch_search)
   uint64_t *wave_clock;   // profiling (MIPGPU_WAVE_TIMING): [workgroup][kClockSlots] cycles per
                           // task of the workgroup's list; else null
 };
 constexpr int kClockSlots = 128;
+// Item queue of one launch: the items are cut into kQueueChunks contiguous chunks, one per
+// XCD (workgroups b and b + 8 share an XCD), each with its own counter (mip_search.hip
+// take_item).
+constexpr int kQueueChunks = 8;
+constexpr int kQueueWords = 16;  // 8 chunk counters, the done counter, padding to 64 bytes
 // CTU variants (mipgpu.cpp ctu_variants): CTUs with the same set of defined CUs share work /
 // fill lists; the lists omit the CUs whose cost the reference leaves undefined.
 constexpr int kMaxCtuVariants = 255;

@@ -8,7 +8,7 @@
 //
 // Work decomposition
 //   workgroup = persistent, 8 waves; takes items = (frame, CTU, quadrant, slice) from a
-//               device-wide counter.  No CU of the 47 shapes straddles a 64x64 quadrant, so
+//               device-wide queue (one counter per XCD chunk, take_item).  No CU of the 47 shapes straddles a 64x64 quadrant, so
 //               an item stages only its quadrant (+1 row above, +4 columns left: the
 //               reference samples) in LDS; the MIP matrices are staged once per workgroup.
 //               CTUs cut by the frame border have their own lists (CUs outside the frame
@@ -1147,7 +1147,7 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
 }
 
 // Next-item prefetch (PF, non-ALT): two quadrant windows in LDS.  The first wave of an item
-// to run out of tasks takes the next item from the device-wide counter and stages its window
+// to run out of tasks takes the next item from the device-wide queue and stages its window
 // into the other buffer while the remaining waves finish theirs, so neither the counter's
 // round trip nor the window's HBM latency stalls the whole workgroup between items (skipping
 // the staging altogether measured +1.2 %).  Taking the next item early would unbalance the
@@ -1158,7 +1158,44 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
 // kernel).  The ALT lattice leaves no LDS for a second window.
 template <bool ALT, bool PF>
 constexpr int kOrgTiles = PF && !ALT ? 2 : 1;
-constexpr int kCounterWords = 8;  // [parity]: next task, finished waves, item, item taken late
+constexpr int kCounterWords = 12;  // [parity]: next task, finished waves, item, item taken late;
+                                   // [8]: chunks this workgroup has found empty (take_item)
+
+// The launch's items in kQueueChunks contiguous chunks (fewer if the grid is smaller), chunk
+// c = [chunk_begin(c), chunk_begin(c + 1)) with its own counter a.queue[c].  Workgroup b
+// takes from chunk b % K first and then from the following ones.  The hardware deals the
+// workgroups round robin over the 8 XCDs, so one chunk's items -- neighbouring quadrants,
+// which share the 128-byte lines of the window's left columns and of the cost rows across
+// the quadrant border -- run on one XCD, close in time, and meet in its L2 (with one counter,
+// neighbours ran on different XCDs: FETCH 2x the frame bytes).  Placement is only a speed
+// matter: any workgroup may take any item.
+__device__ __forceinline__ uint32_t queue_chunks(const SearchArgs &a) { return gridDim.x < a.chunks ? gridDim.x : a.chunks; }
+__device__ __forceinline__ uint32_t chunk_begin(uint32_t nitems, uint32_t c, uint32_t k) {
+  return (uint32_t)((uint64_t)nitems * c / k);
+}
+// One thread of the workgroup at a time (the callers are separated by barriers); *empty (LDS)
+// counts the chunks this workgroup found exhausted, so each costs it one failed atomic.
+__device__ __forceinline__ uint32_t take_item(const SearchArgs &a, uint32_t *empty) {
+  const uint32_t k = queue_chunks(a), g = blockIdx.x % k;
+  for (uint32_t j = *empty; j < k; j++) {
+    const uint32_t c = g + j < k ? g + j : g + j - k;
+    const uint32_t b = chunk_begin(a.nitems, c, k), n = chunk_begin(a.nitems, c + 1, k) - b;
+    const uint32_t i = atomicAdd(a.queue + c, 1u);
+    if (i < n) {
+      *empty = j;
+      return b + i;
+    }
+  }
+  *empty = k;
+  return a.nitems;  // every chunk is exhausted
+}
+// Are many items of the workgroup's own chunk left after `item` (the chunk's head is about
+// one round of its workgroups past the item just taken)?
+__device__ __forceinline__ bool far_from_end(const SearchArgs &a, uint32_t item) {
+  const uint32_t k = queue_chunks(a), g = blockIdx.x % k;
+  const uint32_t b = chunk_begin(a.nitems, g, k), e = chunk_begin(a.nitems, g + 1, k);
+  return item >= b && item + 3 * (gridDim.x / k) < e;
+}
 constexpr uint32_t kTakeItem = 0xffffffffu;  // "take the next item after this one" (PF)
 
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
@@ -1180,19 +1217,22 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 
   // Persistent workgroups (as many as are resident) take items = (frame, CTU, quadrant,
-  // slice) from a device-wide counter, in order: the hardware's static round-robin of
+  // slice) from a device-wide queue (take_item), in order: the hardware's static round-robin of
   // workgroups over XCDs and CUs cannot balance items of unequal cost (edge CTUs).
   // (PF: the first item is taken like a late one, by the loop)
-  if (threadIdx.x < kCounterWords)
-    counters[threadIdx.x] = threadIdx.x != 2 ? 0u : (PF ? kTakeItem : atomicAdd(a.queue, 1u));
+  if (threadIdx.x < kCounterWords) counters[threadIdx.x] = threadIdx.x == 2 && PF ? kTakeItem : 0u;
   __syncthreads();
+  if (!PF) {
+    if (threadIdx.x == 0) counters[2] = take_item(a, counters + 8);
+    __syncthreads();
+  }
   int par = 0;          // workgroup-uniform: parity of the item (window buffer, counter set)
   for (;;) {
     uint32_t *next_task = counters + 4 * par, *finished = next_task + 1;
     uint32_t item = next_task[2];
     bool staged = PF;  // workgroup-uniform: the window of the item is in LDS
     if (PF && item == kTakeItem) {  // near the end of the launch: take the item now
-      if (threadIdx.x == 0) next_task[3] = atomicAdd(a.queue, 1u);
+      if (threadIdx.x == 0) next_task[3] = take_item(a, counters + 8);
       __syncthreads();
       item = next_task[3];
       staged = false;
@@ -1276,9 +1316,10 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
         // Taking the next item before this one is done is worth it only while many items
         // are left: in the last rounds a reserved item would wait for this workgroup while
         // others run dry, so there the next item is taken after the item (kTakeItem).
-        // (the queue head is about one round, gridDim.x items, past this item)
+        // (far_from_end: in the workgroup's own chunk, more than three rounds of its
+        // workgroups left)
         uint32_t n = kTakeItem;
-        if (lane == 0 && item + 3 * gridDim.x < a.nitems) n = atomicAdd(a.queue, 1u);
+        if (lane == 0 && far_from_end(a, item)) n = take_item(a, counters + 8);
         const uint32_t nitem = __builtin_amdgcn_readfirstlane(n);
         if (nitem < a.nitems) {  // (kTakeItem >= nitems)
           const ItemPos np(a, nitem);
@@ -1312,19 +1353,19 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
       __syncthreads();  // every wave is done with the window and the item's counters
       if (threadIdx.x == 0) {
         next_task[0] = 0;
-        next_task[2] = atomicAdd(a.queue, 1u);
+        next_task[2] = take_item(a, counters + 8);
       }
       __syncthreads();  // the next item is in place
     }
     if (PF) par ^= 1;  // (a loop-carried parity costs the ALT kernel ~30 VGPRs)
   }
-  // The last workgroup to leave resets the counter pair for the next launch that uses it
+  // The last workgroup to leave resets the queue's counters for the next launch that uses it
   // (the host never runs two launches on one pair at the same time).
   if (threadIdx.x == 0) {
     __threadfence();
-    if (atomicAdd(a.queue + 1, 1u) == gridDim.x - 1) {
-      atomicExch(a.queue, 0u);
-      atomicExch(a.queue + 1, 0u);
+    if (atomicAdd(a.queue + kQueueChunks, 1u) == gridDim.x - 1) {
+      for (int c = 0; c < kQueueChunks; c++) atomicExch(a.queue + c, 0u);
+      atomicExch(a.queue + kQueueChunks, 0u);
     }
   }
 }
@@ -1430,6 +1471,8 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const long long nitems = (long long)(4 * a.slices) * a.nrange * nframes;
   if (nitems >= 0xffffffffLL) return hipErrorInvalidValue;
   a.nitems = (uint32_t)nitems;
+  const char *qc = getenv("MIPGPU_QUEUE_CHUNKS");  // tuning knob: XCD chunks of the item queue
+  a.chunks = qc && atoi(qc) >= 1 && atoi(qc) <= kQueueChunks ? (uint32_t)atoi(qc) : (uint32_t)kQueueChunks;
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;

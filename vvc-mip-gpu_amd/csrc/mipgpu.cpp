@@ -420,7 +420,8 @@ struct mip_engine {
     int wait(int slot, hipStream_t s) const { return hipStreamWaitEvent(s, e->queue_done[slot], 0) != hipSuccess; }
     int record(int slot, hipStream_t s) const { return hipEventRecord(e->queue_done[slot], s) != hipSuccess; }
     int clear(int slot, hipStream_t s) const {
-      return hipMemsetAsync(e->d_queue + 2 * slot, 0, 2 * sizeof(uint32_t), s) != hipSuccess;
+      return hipMemsetAsync(e->d_queue + mipgpu::kQueueWords * slot, 0, mipgpu::kQueueWords * sizeof(uint32_t), s) !=
+             hipSuccess;
     }
   };
   QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this}};
@@ -590,8 +591,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     ALLOC(e->d_satd, ncost * 4);
   }
   ALLOC(e->d_best, ncu * o.best_k);
-  ALLOC(e->d_queue, 2 * mip_engine::kQueueSlots * sizeof(uint32_t));
-  if (hipMemset(e->d_queue, 0, 2 * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
+  ALLOC(e->d_queue, mipgpu::kQueueWords * mip_engine::kQueueSlots * sizeof(uint32_t));
+  if (hipMemset(e->d_queue, 0, mipgpu::kQueueWords * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail("hipMemset failed"));
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
@@ -771,7 +772,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   if (decisions_only) HIP_TRY(mipgpu::launch_dec_split(sa, nframes, true, s));
   const int slot = e->queue.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
-  a.queue = e->d_queue + 2 * slot;
+  a.queue = e->d_queue + mipgpu::kQueueWords * slot;
   const hipError_t le = mipgpu::launch_search(a, nframes, alt, e->resident[alt ? 1 : 0], s);
   if (le != hipSuccess) {
     e->queue.failed(slot);  // the pair is cleared before its next use
