@@ -19,7 +19,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -97,7 +100,12 @@ class HostStage {
  public:
   static constexpr int kRing = 8;
 
-  ~HostStage() { release(); }
+  ~HostStage() {
+    if (getenv("MIPGPU_STAGE_STATS"))  // diagnostic: where the staging time goes
+      fprintf(stderr, "mipgpu stage: %d threads; upload copies %.1f ms (%.2f GB), download copies %.1f ms (%.2f GB), "
+              "DMA waits %.1f ms\n", threads_, t_up_ * 1e3, b_up_ / 1e9, t_down_ * 1e3, b_down_ / 1e9, t_wait_ * 1e3);
+    release();
+  }
 
   // Page-locked host memory (mip_host_alloc / hipHostRegister) or device memory: transfers
   // run at DMA rate without staging.
@@ -123,7 +131,11 @@ class HostStage {
       if ((e = hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming)) != hipSuccess) return e;
     }
     piece_ = piece;
-    if (!pool_) pool_.reset(new CopyPool(8));
+    if (!pool_) {
+      const char *t = getenv("MIPGPU_COPY_THREADS");  // tuning knob: host copy threads
+      threads_ = t && atoi(t) >= 1 && atoi(t) <= 64 ? atoi(t) : 8;
+      pool_.reset(new CopyPool(threads_));
+    }
     return hipSuccess;
   }
 
@@ -136,7 +148,10 @@ class HostStage {
       int j;
       hipError_t e = take(&j);
       if (e != hipSuccess) return e;
+      const double t0 = now();
       pool_->copy(buf_[j], (const char *)src + o, len);
+      t_up_ += now() - t0;
+      b_up_ += len;
       if ((e = hipMemcpyAsync((char *)dst_dev + o, buf_[j], len, hipMemcpyHostToDevice, s)) != hipSuccess ||
           (e = hipEventRecord(ev_[j], s)) != hipSuccess)
         return e;
@@ -188,9 +203,16 @@ class HostStage {
 
   hipError_t complete_front() {
     const Piece p = fifo_.front();
+    const double t0 = now();
     const hipError_t e = hipEventSynchronize(ev_[p.ring]);
+    const double t1 = now();
+    t_wait_ += t1 - t0;
     if (e != hipSuccess) return e;
-    if (p.dst) pool_->copy(p.dst, buf_[p.ring], p.bytes);
+    if (p.dst) {
+      pool_->copy(p.dst, buf_[p.ring], p.bytes);
+      t_down_ += now() - t1;
+      b_down_ += p.bytes;
+    }
     fifo_.pop_front();
     return hipSuccess;
   }
@@ -216,6 +238,11 @@ class HostStage {
     next_ = 0;
   }
 
+  static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  int threads_ = 0;
+  double t_up_ = 0, t_down_ = 0, t_wait_ = 0, b_up_ = 0, b_down_ = 0;
   char *buf_[kRing] = {};
   hipEvent_t ev_[kRing] = {};
   size_t piece_ = 0;
