@@ -899,7 +899,18 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // page-locked host memory (mip_host_alloc); pageable buffers go through the engine's
   // page-locked bounce ring (host_stage.h), their downloads finished by mip_wait.
   const int nslots = e->opts.max_batch >= 16 ? 4 : (e->opts.max_batch >= 2 ? 2 : 1);
-  const int sb = e->opts.max_batch / nslots;
+  int sb = e->opts.max_batch / nslots;
+  // Full tables to the host (PCIe-bound): chunks of at most ~1 GiB of downloads, so the
+  // first download starts early and, for pageable outputs, the bounce ring's copy-out keeps
+  // up (1080p, 8 calls of 128 frames: 96-frame chunks 831 frames/s pageable, 32-frame 892,
+  // 16-frame 1018; page-locked 990 / 963 / 1036).  Decisions only keeps the larger chunks
+  // (its rate is the search's, whose launches are more efficient with more frames).
+  const size_t down_per_frame = (size_t)((costs_out ? 1 : 0) + (sad_out ? 1 : 0) + (satd_out ? 1 : 0)) * cpf * 4;
+  if (down_per_frame) {
+    const char *cm = getenv("MIPGPU_CHUNK_MB");  // tuning knob: download bytes per chunk
+    const size_t cap = (size_t)(cm && atoi(cm) > 0 ? atoi(cm) : 1024) << 20;
+    sb = std::max(1, std::min<int>(sb, (int)(cap / down_per_frame)));
+  }
   const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
   const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
   const bool pin_in = mipgpu::HostStage::pinned(frames) && (!refs_or_null || mipgpu::HostStage::pinned(refs_or_null));
