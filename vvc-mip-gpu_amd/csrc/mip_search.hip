@@ -222,6 +222,28 @@ struct RefTile {
   __device__ __forceinline__ int left(int x, int y) const {     // x = 4i - 1
     return LAT ? t[16 * kLatRowPitch + ((x + 1) >> 2) * kLatColPitch + y + 1] : t[tidx(x, y)] - (int)kBiasD[0][3];
   }
+  template <int PH>  // PH = y & 3 (the bias of a reference column does not depend on it)
+  __device__ __forceinline__ int left_ph(int x, int y) const { return left(x, y); }
+};
+
+// Transposed view of a reference tile, for classes searched as their transpose (TR tasks,
+// see run_task): (x, y) here is (y, x) in the tile, so this view's top row is the tile's left
+// column and its left column the tile's top row.
+template <bool LAT>
+struct RefTileT {
+  RefTile<LAT> r;
+  template <int PH>
+  __device__ __forceinline__ int top(int x, int y) const { return r.left(y, x); }
+  __device__ __forceinline__ uint2 top4(int x, int y) const {
+    return make_uint2((uint32_t)r.left(y, x) | (uint32_t)r.left(y, x + 1) << 16,
+                      (uint32_t)r.left(y, x + 2) | (uint32_t)r.left(y, x + 3) << 16);
+  }
+  template <int PH>  // PH = y & 3: the tile column y & 3 of the tile row's bias
+  __device__ __forceinline__ int left_ph(int x, int y) const { return r.template top<PH>(y, x); }
+  __device__ __forceinline__ int left(int x, int y) const {  // runtime bias (PAD classes only)
+    const int ph = y & 3;
+    return ph == 0 ? left_ph<0>(x, y) : ph == 1 ? left_ph<1>(x, y) : ph == 2 ? left_ph<2>(x, y) : left_ph<3>(x, y);
+  }
 };
 
 __device__ __forceinline__ uint2 lds_row4(const uint16_t *tile, int x, int y) {
@@ -235,14 +257,15 @@ struct CuPos {
   int padT, padL;  // padding values, intra.cl:102-106, 238-242
 };
 
-template <bool LAT>
-__device__ __forceinline__ CuPos cu_pos(const Job &j, int fx0, int fy0, const RefTile<LAT> &rt) {
+// TR: the CU's transpose -- origin (ly, lx) in the transposed view (fx0 / fy0 swapped too).
+template <bool TR, class RT>
+__device__ __forceinline__ CuPos cu_pos(const Job &j, int fx0, int fy0, const RT &rt) {
   CuPos c;
-  c.lx = j.lx;
-  c.ly = j.ly;
-  c.top = fy0 + c.ly > 0;
-  c.left = fx0 + c.lx > 0;
-  c.padT = c.left ? rt.left(c.lx - 1, c.ly) : 512;  // top edge: sample (x-1, 0)
+  c.lx = TR ? j.ly : j.lx;
+  c.ly = TR ? j.lx : j.ly;
+  c.top = (TR ? fx0 : fy0) + c.ly > 0;
+  c.left = (TR ? fy0 : fx0) + c.lx > 0;
+  c.padT = c.left ? rt.template left_ph<0>(c.lx - 1, c.ly) : 512;  // top edge: sample (x-1, 0)
   c.padL = c.top ? rt.template top<0>(c.lx, c.ly - 1) : 512;    // left edge: sample (0, y-1)
   return c;
 }
@@ -253,8 +276,8 @@ __device__ __forceinline__ CuPos cu_pos(const Job &j, int fx0, int fy0, const Re
 // transposed orientation (redL, redT) (intra.cl:417-418) is the same entry read with its
 // two 8-byte halves swapped; sizeId 0 stores (T0 T1 L0 L1 | L0 L1 T0 T1) for that.
 // The coefficient tables (mip_kernels.h) absorb p = b - b0, p_0 and the bias.
-template <int W, int H, bool LAT>
-__device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> &rt, uint8_t *entry) {
+template <int W, int H, class RT>
+__device__ __forceinline__ void write_inputs(const CuPos &c, const RT &rt, uint8_t *entry) {
   using G = Geo<W, H>;
   constexpr int dfT = W / G::RBS, l2T = ilog2c(dfT), rndT = dfT > 1 ? dfT / 2 : 0;
   constexpr int dfL = H / G::RBS, l2L = ilog2c(dfL), rndL = dfL > 1 ? dfL / 2 : 0;
@@ -276,8 +299,10 @@ __device__ __forceinline__ void write_inputs(const CuPos &c, const RefTile<LAT> 
     }
     redT[i] = c.top ? (s + rndT) >> l2T : c.padT;
     uint32_t l = 0;
-#pragma unroll
-    for (int t = 0; t < dfL; t++) l += rt.left(c.lx - 1, c.ly + i * dfL + t);
+    static_for<dfL>([&](auto t_c) {  // c.ly % 4 == 0: the row phase is i * dfL + t
+      constexpr int off = i * dfL + decltype(t_c)::value;
+      l += rt.template left_ph<off & 3>(c.lx - 1, c.ly + off);
+    });
     redL[i] = c.left ? (l + rndL) >> l2L : c.padL;
   });
   constexpr uint32_t kBias = 0x64006400u;  // f16 1024.0 in both halves
@@ -494,6 +519,86 @@ struct PackedAcc {
   }
 };
 
+// ---- transposed classes (TR) ----------------------------------------------------------------
+// A wide CU W x H is searched as its transpose H x W (run_task): the transposed view's 4x4 block
+// row I is the tile's block column I, so the original samples arrive one per register (OrigT)
+// and carry the staged bias of the TILE position, kBiasD[c & 1][I] at view position (I, c).
+// The block transform is the same 2-D Hadamard with the two butterfly stages swapped: the
+// residual rows are kept raw and the butterflies of the tile's rows (view columns) run first
+// (block_finish / pair_finish for BlockAccTr), which reproduces exactly the biased values the
+// untransposed path builds, so the folds and the SATD rounding are unchanged.  SAD and SATD
+// of a block are invariant under transposition.
+struct OrigT {
+  uint32_t v[4];  // view row: columns x..x+3 = tile rows, one staged (biased) sample each
+};
+
+struct BlockAccTr {
+  uint32_t t[16];  // raw biased residuals, view position (I, c) at 4 * I + c
+  uint32_t pos;
+};
+
+template <int I>
+__device__ __forceinline__ void residual_row(const s2 (&prow)[4], const OrigT &o, uint32_t (&d)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; c++) d[c] = as_u32(s2{(short)o.v[c], (short)o.v[c]} - prow[c]);
+}
+
+template <int I>
+__device__ __forceinline__ void block_row(BlockAccTr &b, const s2 (&prow)[4], const OrigT &o) {
+  uint32_t d[4];
+  residual_row<I>(prow, o, d);
+  uint32_t p = 0;
+  static_for<4>([&](auto c_c) {
+    constexpr int c = decltype(c_c)::value;
+    constexpr unsigned short B = (unsigned short)kBiasD[c & 1][I];
+    p += as_u32(__builtin_elementwise_sub_sat(as_u2(d[c]), (u2){B, B}));
+    b.t[4 * I + c] = d[c];
+  });
+  b.pos = I == 0 ? p : b.pos + p;
+}
+
+// The tile-row butterflies (view columns) of raw residuals -> the row-transformed layout of
+// block_row (tile row r at 4 * r + k).
+__device__ __forceinline__ void rows_transform_tr(const uint32_t (&raw)[16], uint32_t (&t)[16]) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t e0 = raw[r], e1 = raw[4 + r], e2 = raw[8 + r], e3 = raw[12 + r];
+    const uint32_t s0 = e0 + e1, s1 = e0 - e1, s2_ = e2 + e3, s3 = e2 - e3;
+    t[4 * r + 0] = s0 + s2_;
+    t[4 * r + 1] = s1 + s3;
+    t[4 * r + 2] = s0 - s2_;
+    t[4 * r + 3] = s1 - s3;
+  }
+}
+
+__device__ __forceinline__ void block_finish(const BlockAccTr &b, u2 &sad, u2 &satd) {
+  BlockAcc r;
+  rows_transform_tr(b.t, r.t);
+  r.pos = b.pos;
+  block_finish(r, sad, satd);
+}
+
+// Paired walk, TR: as pair_row with the tile-position biases; rows kept raw.
+template <int I>
+__device__ __forceinline__ void pair_row_tr(const uint32_t *dA, const uint32_t (&dB)[4], uint32_t (&t0)[16],
+                                            uint32_t (&t1)[16], PairAcc &acc) {
+  static_for<4>([&](auto c_c) {
+    constexpr int c = decltype(c_c)::value;
+    const uint32_t m0 = __builtin_amdgcn_perm(dB[c], dA[c], 0x05040100u);  // (A.mode0, B.mode0)
+    const uint32_t m1 = __builtin_amdgcn_perm(dB[c], dA[c], 0x07060302u);  // (A.mode1, B.mode1)
+    acc.sad0 = __builtin_amdgcn_sad_u16(m0, splat32(kBiasD[c & 1][I]), acc.sad0);
+    acc.sad1 = __builtin_amdgcn_sad_u16(m1, splat32(kBiasD[c & 1][I]), acc.sad1);
+    t0[4 * I + c] = m0;
+    t1[4 * I + c] = m1;
+  });
+}
+
+__device__ __forceinline__ uint32_t pair_finish_tr(const uint32_t (&raw)[16], uint32_t T) {
+  uint32_t t[16];
+  rows_transform_tr(raw, t);
+  return pair_finish(t, T);
+}
+
 // Reduced prediction of the lane's CU in the wave scratch: both modes of the pair per dword,
 // stored position (k, kx) at k*R + kx (rows offset by `k0` for the second half of a chunked
 // class).
@@ -576,6 +681,8 @@ __device__ __forceinline__ void anchor_row(const RED &red, int k, int x0, s2 (&a
 // pairs for 4-row CUs, re-read from LDS otherwise (register budget).
 template <int H>
 struct OrigRows {
+  static constexpr bool TR = false;
+  using Block = BlockAcc;
   static constexpr bool CACHED = H <= 4;
   uint2 r[CACHED ? H : 1];
   const uint16_t *tile;
@@ -595,16 +702,36 @@ struct OrigRows {
   }
 };
 
+// Original samples of a TR lane's strip: view row i = tile column, re-read per mode pair.
+template <int H>
+struct OrigRowsT {
+  static constexpr bool TR = true;
+  using Block = BlockAccTr;
+  const uint16_t *tile;
+  int x, y;  // view coordinates of the strip's first sample
+  __device__ __forceinline__ void load(const uint16_t *t, int xx, int yy) {
+    tile = t;
+    x = xx;
+    y = yy;
+  }
+  __device__ __forceinline__ OrigT operator()(int i) const {
+    OrigT o;
+#pragma unroll
+    for (int k = 0; k < 4; k++) o.v[k] = tile[tidx(y + i, x + k)];
+    return o;
+  }
+};
+
 // Walk one strip of one CU for one mode pair over upsampling windows [k0, k1) (rows for
 // UV == 1 and 4x4): prediction rows (upsampling, intra.cl:815-912) streamed through the
 // block transform.  `prev` is the anchor row above window k0 (vertical pass state).
-template <int W, int H, int V, bool LAT, class RED, class ACC>
-__device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &rt, const OrigRows<H> &orig,
-                                           const RED &red, int x0, int k0, int k1, s2 (&prev)[4], ACC &acc) {
+template <int W, int H, int V, class ORIG, class RED, class ACC>
+__device__ __forceinline__ void walk_strip(const ORIG &orig, const RED &red, int x0, int k0, int k1, s2 (&prev)[4],
+                                           ACC &acc) {
   using G = Geo<W, H, V>;
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
-    BlockAcc b;
+    typename ORIG::Block b;
     static_for<4>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
       s2 prow[4];
@@ -620,7 +747,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
 #pragma unroll
     for (int bi = 0; bi < G::KV / 4; bi++) {
       const int by = k0 / 4 + bi;
-      BlockAcc b;
+      typename ORIG::Block b;
       static_for<4>([&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
         s2 prow[4];
@@ -640,7 +767,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
 #pragma unroll kUnroll
     for (int bi = 0; bi < NBLK; bi++) {
       const int by = k0 / 2 + bi;
-      BlockAcc b;
+      typename ORIG::Block b;
       static_for<2>([&](auto hh_c) {
         constexpr int hh = decltype(hh_c)::value;
         const int k = 2 * by + hh;
@@ -678,7 +805,7 @@ __device__ __forceinline__ void walk_strip(const CuPos &c, const RefTile<LAT> &r
       }
       static_for<NB>([&](auto bi_c) {
         constexpr int bi = decltype(bi_c)::value;
-        BlockAcc b;
+        typename ORIG::Block b;
         static_for<4>([&](auto i_c) {
           constexpr int i = decltype(i_c)::value, o = 4 * bi + i + 1;
           s2 prow[4];
@@ -709,8 +836,8 @@ template <int W, int H, int V>
 constexpr bool kPaired = Geo<W, H, V>::SID != 0 && W * H > 32 && V == kClassV[size_class(W, H)] &&
                          ((Geo<W, H, V>::CHUNKED ? 4 * Geo<W, H, V>::UV : Geo<W, H, V>::KV * Geo<W, H, V>::UV) / 4) % 2 == 0;
 
-template <int W, int H, int V, class RED>
-__device__ __forceinline__ void walk_pairs(const OrigRows<H> &orig, const RED &red, int x0, int k0, s2 (&prev)[4],
+template <int W, int H, int V, class ORIG, class RED>
+__device__ __forceinline__ void walk_pairs(const ORIG &orig, const RED &red, int x0, int k0, s2 (&prev)[4],
                                            PairAcc &acc) {
   using G = Geo<W, H, V>;
   constexpr int ROWS = G::CHUNKED ? 4 * G::UV : G::KV * G::UV;  // CU rows of this call
@@ -732,7 +859,8 @@ __device__ __forceinline__ void walk_pairs(const OrigRows<H> &orig, const RED &r
       } else {
         uint32_t dB[4];
         residual_row<i - 4>(prow, orig(yb + i), dB);
-        pair_row<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
+        if constexpr (ORIG::TR) pair_row_tr<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
+        else pair_row<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
       }
     };
     if constexpr (G::UV == 1) {
@@ -786,8 +914,13 @@ __device__ __forceinline__ void walk_pairs(const OrigRows<H> &orig, const RED &r
         for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
       });
     }
-    acc.t0 = pair_finish(t0, acc.t0);
-    acc.t1 = pair_finish(t1, acc.t1);
+    if constexpr (ORIG::TR) {
+      acc.t0 = pair_finish_tr(t0, acc.t0);
+      acc.t1 = pair_finish_tr(t1, acc.t1);
+    } else {
+      acc.t0 = pair_finish(t0, acc.t0);
+      acc.t1 = pair_finish(t1, acc.t1);
+    }
   }
 }
 
@@ -913,9 +1046,28 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
-template <int W, int H, int V, bool LAT, bool DEC>
-__device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, const WaveTask &task, int lane_in) {
+template <bool TR, bool LAT>
+struct ViewOf {
+  using type = RefTile<LAT>;
+  static __device__ __forceinline__ type make(const RefTile<LAT> &r) { return r; }
+};
+template <bool LAT>
+struct ViewOf<true, LAT> {
+  using type = RefTileT<LAT>;
+  static __device__ __forceinline__ type make(const RefTile<LAT> &r) { return RefTileT<LAT>{r}; }
+};
+
+// One task: CUs of class W x H (TR: the task's CUs are H x W and are searched as their
+// transpose W x H -- the same MIP prediction transposed for the other orientation of each
+// mode (intra.cl:417-418, 485: a transposed mode swaps the boundary halves and stores the
+// output transposed), so mode pair q of the view is the CU's pair (q + MODES / 2) mod MODES;
+// single-direction upsampling is the same interpolation along the other axis, and SAD / SATD
+// do not change under transposition).  Wide CUs (W > H) cost up to 1.5x the VALU of their
+// tall transposes (profiles/r03_shape_pmc.txt).
+template <int W, int H, int V, bool LAT, bool DEC, bool TR = false>
+__device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_tile, const WaveTask &task, int lane_in) {
   using G = Geo<W, H, V>;
+  const typename ViewOf<TR, LAT>::type rt = ViewOf<TR, LAT>::make(rt_tile);
   const int lane = opaque(lane_in);
   const SearchArgs &a = *x.a;
   const int ncu = task.ncu;
@@ -926,15 +1078,15 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
   const bool active = slot < ncu;
   const int cs = min(slot, ncu - 1);
   const Job job = jobs[cs];
-  const CuPos c = cu_pos(job, x.fx0, x.fy0, rt);
+  const CuPos c = cu_pos<TR>(job, x.fx0, x.fy0, rt);
 
   // ---- per-CU MFMA inputs of both orientations -> wave table
   if (lane < ncu) {
     const Job jb = jobs[lane];
-    const CuPos cj = cu_pos(jb, x.fx0, x.fy0, rt);
+    const CuPos cj = cu_pos<TR>(jb, x.fx0, x.fy0, rt);
     write_inputs<W, H>(cj, rt, x.wave + lane * kEntryBytes);
   }
-  OrigRows<H> orig;
+  std::conditional_t<TR, OrigRowsT<H>, OrigRows<H>> orig;
   orig.load(x.org, c.lx + x0, c.ly);
   const size_t cbase = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
   const uint32_t *mine = reinterpret_cast<const uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
@@ -981,21 +1133,21 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       }
       walk_pairs<W, H, V>(orig, red, x0, k0, prev, acc);
     } else if constexpr (G::CHUNKED) {
-      walk_strip<W, H, V>(c, rt, orig, red, x0, 0, 4, prev, acc);
+      walk_strip<W, H, V>(orig, red, x0, 0, 4, prev, acc);
       wave_lds_sync();
       phase_a<W, H, V>(x, lane, ncu, q, 1);
       wave_lds_sync();
       const Red<G::R, G::RP> red_hi{mine, -4};  // chunk 1 holds reduced rows 4..7
-      walk_strip<W, H, V>(c, rt, orig, red_hi, x0, 4, 8, prev, acc);  // prev carries anchor row 3
+      walk_strip<W, H, V>(orig, red_hi, x0, 4, 8, prev, acc);  // prev carries anchor row 3
     } else if constexpr (G::SID == 0) {
-      walk_strip<W, H, V>(c, rt, orig, red, x0, 0, 4, prev, acc);
+      walk_strip<W, H, V>(orig, red, x0, 0, 4, prev, acc);
     } else {
       // row part v: windows [v*KV, (v+1)*KV) (rows when UV == 1)
       const int k0 = G::V > 1 ? v * G::KV : 0;
       if constexpr (G::V > 1 && G::UV > 1) {
         if (k0 > 0) anchor_row<W, H>(red, k0 - 1, x0, prev);
       }
-      walk_strip<W, H, V>(c, rt, orig, red, x0, k0, k0 + G::KV, prev, acc);
+      walk_strip<W, H, V>(orig, red, x0, k0, k0 + G::KV, prev, acc);
     }
     wave_lds_sync();  // the scratch is rewritten by the next pair
     // ---- combine strips and row parts of one CU (adjacent lanes) into its last lane
@@ -1025,10 +1177,12 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt, c
       c1 = min(2 * (int)sad1, (int)satd1);
     }
     if (active && sub == GS - 1) {
-      const size_t idx = cbase + 2 * q;  // every CU of a task lies inside the frame (build_work)
+      // the CU's modes of view pair q (TR: the other orientation)
+      const int mq = TR ? (2 * q < G::MODES ? 2 * q + G::MODES : 2 * q - G::MODES) : 2 * q;
+      const size_t idx = cbase + mq;  // every CU of a task lies inside the frame (build_work)
       if constexpr (DEC) {
         // costs < 2^23 (256 blocks x 32736): the packed order is cost, then the lower mode
-        best = min(best, min((uint32_t)c0 << 5 | (uint32_t)(2 * q), (uint32_t)c1 << 5 | (uint32_t)(2 * q + 1)));
+        best = min(best, min((uint32_t)c0 << 5 | (uint32_t)mq, (uint32_t)c1 << 5 | (uint32_t)(mq + 1)));
       } else {
         *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
         if (a.sad) *reinterpret_cast<int2 *>(a.sad + idx) = make_int2(sad0, sad1);
@@ -1301,6 +1455,16 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
           // row-part variants for remainder tasks (mip_kernels.h)
           MIP_CASE(17, 32, 8) MIP_CASE(18, 16, 16) MIP_CASE(19, 16, 8) MIP_CASE(20, 8, 16)
 #undef MIP_CASE
+#define MIP_CASE_TR(idx, W, H)                                                    \
+  case idx:                                                                       \
+    static_assert(kClassW[idx] == W && kClassH[idx] == H && kClassTR[idx], "class table"); \
+    if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)                              \
+      run_task<W, H, kClassV[idx], ALT, DEC, true>(x, rt, task, lane);            \
+    break;
+          // transposed classes: wide CUs searched as their transposes
+          MIP_CASE_TR(21, 4, 32) MIP_CASE_TR(22, 4, 16) MIP_CASE_TR(23, 4, 8) MIP_CASE_TR(24, 8, 32)
+          MIP_CASE_TR(25, 8, 16) MIP_CASE_TR(26, 8, 16)
+#undef MIP_CASE_TR
           default: break;
         }
         if (clk && lane == 0 && t < kClockSlots) clk[t] = __builtin_readcyclecounter() - c0;

@@ -145,6 +145,13 @@ double cut_factor() {
   return e && atof(e) > 0 ? atof(e) : 2.0;
 }
 
+// Wide CUs (32x4, 16x4, 8x4, 32x8, 16x8) searched as their tall transposes (transposed
+// classes, mip_kernels.h); MIPGPU_TRANSPOSE=0 (A/B knob) searches them as they are.
+bool transpose_wide() {
+  const char *e = getenv("MIPGPU_TRANSPOSE");
+  return !(e && *e == '0');
+}
+
 // MIPGPU_NO_PAIRS=1 (profiling knob): tasks keep their prologue but search no mode pair.
 bool no_pairs() {
   const char *e = getenv("MIPGPU_NO_PAIRS");
@@ -251,7 +258,8 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
     for (int s = 0; s < MIP_NUM_SHAPES; shape_cu0 += kShapes[s].ncu, s++) {
       if (!shape_selected(s)) continue;
       const mip_shape_desc &sd = kShapes[s];
-      const int cls = mipgpu::size_class(sd.w, sd.h);
+      int cls = mipgpu::size_class(sd.w, sd.h);
+      if (transpose_wide() && mipgpu::kClassTransposed[cls] >= 0) cls = mipgpu::kClassTransposed[cls];
       for (int cu = 0; cu < sd.ncu; cu++) {
         const int x = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
         if (x / 64 != (q & 1) || y / 64 != (q >> 1)) continue;
@@ -266,7 +274,7 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
       }
     }
     double total = 0;
-    for (int cls = 0; cls < mipgpu::kNumBaseClasses; cls++) {
+    for (int cls = 0; cls < mipgpu::kNumClasses; cls++) {
       const std::vector<mipgpu::Job> &v = cls_cus[cls];
       if (v.empty()) continue;
       const int nv = (int)v.size(), slots = mipgpu::class_slots(cls);
