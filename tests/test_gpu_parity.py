@@ -467,6 +467,31 @@ def test_device_decisions_only_fused_argmin(gpu_available, w, h, filt, k):
             eng.search_device(d[:1], costs=False, best_mode=bm[:1])
 
 
+@pytest.mark.parametrize("w,h,filt,k", [(392, 264, None, 0), (416, 240, "filterFrame_1d_int_5x5", 2)])
+def test_transposed_classes_equal_direct_search(gpu_available, monkeypatch, w, h, filt, k):
+    """Wide single-direction CUs (32x4, 16x4, 8x4, 32x8, 16x8) are searched as their tall
+    transposes (transposed classes, mip_kernels.h).  Engines built with MIPGPU_TRANSPOSE=0
+    (searched as they are) and =1 (default) must give identical cost / SAD / SATD tables and
+    decisions, equal to the oracle's; partial CTUs on both axes and, at 416x240 with a
+    separable filter, the fixup CUs."""
+    frames = synth_frames(w, h, 2, 0x7A + w, 1)
+    out = {}
+    for t in ("0", "1"):
+        monkeypatch.setenv("MIPGPU_TRANSPOSE", t)
+        with MipEngine(w, h, max_batch=2, filter=filt, kernel_idx=k, want_sad_satd=True) as eng:
+            out[t] = eng.search(frames, best=True, sad_satd=True)
+            out[t + "dec"] = eng.search(frames, costs=False, best=True)
+    for key in ("cost", "sad", "satd", "best_mode", "best_cost"):
+        assert np.array_equal(out["0"][key], out["1"][key]), key
+    for key in ("best_mode", "best_cost"):
+        assert np.array_equal(out["0dec"][key], out["1"][key]), key
+    for f in range(2):
+        refs = O.filter_frame(frames[f], filt, k) if filt else None
+        cost, sad, satd = O.search(frames[f], refs, want_sad_satd=True)
+        assert np.array_equal(out["1"]["cost"][f], cost)
+        assert np.array_equal(out["1"]["sad"][f], sad) and np.array_equal(out["1"]["satd"][f], satd)
+
+
 def test_decisions_only_full_size_matches_table_argmin(gpu_available):
     """1080p (the bench size), 2 frames: the fused decisions-only search gives exactly the
     decision lists of the full cost table (best_mode_kernel over it)."""
