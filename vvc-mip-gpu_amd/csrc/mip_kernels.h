@@ -29,23 +29,24 @@ struct WaveTask {
 // strip so that a task still fills the wave); 17-20 are variants with more row parts, used
 // for the remainder group of a class whose CU count per quadrant is not a multiple of its
 // task size (e.g. 28 CUs of 32x8 = 3 tasks of 8 + one task of 4 CUs with V = 2; 84 CUs of
-// 8x16 = 2 tasks of 32 + three tasks of 7, 7, 6 CUs with V = 4).  21-26 are *transposed*
+// 8x16 = 2 tasks of 32 + three tasks of 7, 7, 6 CUs with V = 4; 12 CUs of 32x16 = one task of
+// 8 + one task of 4 with V = 2, classes 27-28).  21-26 are *transposed*
 // classes (kClassTR): tasks of wide CUs (32x4, 16x4, 8x4, 32x8, 16x8 -- one upsampling
 // direction only) searched as their tall transposes W x H listed here (mip_search.hip
 // run_task; the CU position sets of a size and its transpose are transposes of each other).
-constexpr int kNumClasses = 27;
+constexpr int kNumClasses = 29;
 constexpr int kNumBaseClasses = 17;
 constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 16, 4, 8, 8, 4, 4, 32, 16, 16, 8,
-                                      4, 4, 4, 8, 8, 8};
+                                      4, 4, 4, 8, 8, 8, 32, 16};
 constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4, 8, 16, 8, 16,
-                                      32, 16, 8, 32, 16, 16};
-constexpr int kClassV[kNumClasses] = {4, 2, 2, 4, 1, 1, 2, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2, 4,
-                                      2, 2, 1, 1, 1, 4};
+                                      32, 16, 8, 32, 16, 16, 16, 32};
+constexpr int kClassV[kNumClasses] = {4, 2, 1, 2, 1, 1, 1, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2, 4,
+                                      2, 2, 1, 1, 1, 4, 2, 4};
 constexpr bool kClassTR[kNumClasses] = {false, false, false, false, false, false, false, false, false, false, false,
                                         false, false, false, false, false, false, false, false, false, false,
-                                        true, true, true, true, true, true};
-constexpr int kClassVariant[kNumClasses] = {-1, -1, -1, -1, 17, -1, 18, 19, 20, -1, -1, -1, -1, -1, -1, -1, -1,
-                                            -1, -1, -1, -1, -1, -1, -1, -1, 26, -1};  // remainder-task class
+                                        true, true, true, true, true, true, false, false};
+constexpr int kClassVariant[kNumClasses] = {-1, -1, 27, 28, 17, -1, 18, 19, 20, -1, -1, -1, -1, -1, -1, -1, -1,
+                                            -1, -1, -1, -1, -1, -1, -1, -1, 26, -1, -1, -1};  // remainder-task class
 // base class -> its transposed class (-1: searched as it is)
 constexpr int kClassTransposed[kNumBaseClasses] = {-1, -1, -1, -1, 24, -1, -1, 25, -1, 21, -1, 22, -1, -1, 23, -1, -1};
 constexpr int size_class(int w, int h) {  // base class of a CU size

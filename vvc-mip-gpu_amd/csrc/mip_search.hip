@@ -1454,6 +1454,7 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
           MIP_CASE(16, 4, 4)
           // row-part variants for remainder tasks (mip_kernels.h)
           MIP_CASE(17, 32, 8) MIP_CASE(18, 16, 16) MIP_CASE(19, 16, 8) MIP_CASE(20, 8, 16)
+          MIP_CASE(27, 32, 16) MIP_CASE(28, 16, 32)
 #undef MIP_CASE
 #define MIP_CASE_TR(idx, W, H)                                                    \
   case idx:                                                                       \
