@@ -394,6 +394,34 @@ def test_pageable_and_pinned_host_buffers_agree(gpu_available):
     assert np.array_equal(pinned["cost"][3], O.search(frames[3]))
 
 
+def test_async_calls_with_different_chunk_sizes(gpu_available):
+    """Asynchronous host calls whose chunk sizes differ (call lengths 5 / 7 / 3 / 11 frames are
+    cut into equal chunks of up to a slot's 4 frames; decisions-only and full-table calls
+    interleaved) all in flight at once: every chunk uses its slot's fixed region of the engine
+    buffers, ordered by the slot's events, so each call's outputs equal a synchronous search
+    of the same frames."""
+    w, h = 392, 264
+    frames = synth_frames(w, h, 26, 0xC5A, 0)
+    with MipEngine(w, h, max_batch=16, want_sad_satd=True) as eng:
+        want = eng.search(frames, best=True, sad_satd=True)
+        spans = [(0, 5, "full"), (5, 12, "dec"), (12, 15, "sad"), (15, 26, "dec"), (0, 11, "full")]
+        tickets = []
+        for a0, a1, kind in spans:
+            if kind == "dec":
+                tickets.append(eng.search_async(frames[a0:a1], costs=False, best=True))
+            else:
+                tickets.append(eng.search_async(frames[a0:a1], best=True, sad_satd=kind == "sad"))
+        outs = [eng.wait(t) for t in tickets]
+    for (a0, a1, kind), o in zip(spans, outs):
+        assert np.array_equal(o["best_mode"], want["best_mode"][a0:a1]), (a0, a1, kind)
+        assert np.array_equal(o["best_cost"], want["best_cost"][a0:a1]), (a0, a1, kind)
+        if kind != "dec":
+            assert np.array_equal(o["cost"], want["cost"][a0:a1]), (a0, a1, kind)
+        if kind == "sad":
+            assert np.array_equal(o["sad"], want["sad"][a0:a1]) and np.array_equal(o["satd"], want["satd"][a0:a1])
+    assert np.array_equal(want["cost"][7], O.search(frames[7]))
+
+
 def test_dropped_ticket_waits(gpu_available):
     """A search_async ticket dropped without wait(): its finaliser waits, so the output and
     input arrays it keeps alive are not freed while the engine's copies use them; the

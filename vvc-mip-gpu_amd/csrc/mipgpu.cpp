@@ -907,7 +907,11 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // page-locked host memory (mip_host_alloc); pageable buffers go through the engine's
   // page-locked bounce ring (host_stage.h), their downloads finished by mip_wait.
   const int nslots = e->opts.max_batch >= 16 ? 4 : (e->opts.max_batch >= 2 ? 2 : 1);
-  int sb = e->opts.max_batch / nslots;
+  // a slot is a fixed region of slot_cap frames of the engine buffers (chunk sizes differ
+  // between calls -- outputs requested, call length -- but a slot's region never moves, so
+  // the per-slot events order every reuse of it)
+  const int slot_cap = e->opts.max_batch / nslots;
+  int sb = slot_cap;
   // Full tables to the host (PCIe-bound): chunks of at most ~1 GiB of downloads, so the
   // first download starts early and, for pageable outputs, the bounce ring's copy-out keeps
   // up (1080p, 8 calls of 128 frames: 96-frame chunks 831 frames/s pageable, 32-frame 892,
@@ -918,6 +922,10 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     const char *cm = getenv("MIPGPU_CHUNK_MB");  // tuning knob: download bytes per chunk
     const size_t cap = (size_t)(cm && atoi(cm) > 0 ? atoi(cm) : 1024) << 20;
     sb = std::max(1, std::min<int>(sb, (int)(cap / down_per_frame)));
+  }
+  {  // equal chunks: a short last chunk would leave the search waiting for the next upload
+    const int nch = (nframes + sb - 1) / sb;
+    sb = (nframes + nch - 1) / nch;
   }
   const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
   const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
@@ -943,7 +951,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     const uint64_t k = e->host_chunks++;
     const int sl = (int)(k % nslots);
     const bool reuse = k >= (uint64_t)nslots;  // the slot served chunk k - nslots (this or an earlier call)
-    const size_t fo = (size_t)sl * sb;  // first engine frame slot of this chunk
+    const size_t fo = (size_t)sl * slot_cap;  // first engine frame of this chunk's slot
     uint16_t *d_frames = e->d_frames + fo * fs;
     if (reuse) HIP_TRY(hipStreamWaitEvent(up, e->slot_comp[sl], 0));
     if (e->trace) {
