@@ -520,6 +520,24 @@ def test_transposed_classes_equal_direct_search(gpu_available, monkeypatch, w, h
         assert np.array_equal(out["1"]["sad"][f], sad) and np.array_equal(out["1"]["satd"][f], satd)
 
 
+@pytest.mark.parametrize("slices", [1, 2, 3, 4])
+def test_slice_counts_agree(gpu_available, slices):
+    """Engines with a fixed number of workgroups per CTU quadrant (mip_opts.slices_per_ctu:
+    the task lists are cut into more pair ranges, so more CUs are split over tasks -- the
+    decisions-only path's packed atomicMin entries) give the oracle's tables and argmins,
+    with alternative references (fixup CUs) at a width that is not a multiple of 128."""
+    w, h, filt, k = 416, 240, "filterFrame_2d_int_quarterCtu", 1
+    frames = synth_frames(w, h, 2, 0x51C + slices, 1)
+    with MipEngine(w, h, max_batch=2, filter=filt, kernel_idx=k, slices_per_ctu=slices) as eng:
+        full = eng.search(frames, best=True)
+        dec = eng.search(frames, costs=False, best=True)
+    for f in range(2):
+        cost = O.search(frames[f], O.filter_frame(frames[f], filt, k))
+        assert np.array_equal(full["cost"][f], cost), f
+        bm, bc = layout.best_modes(cost, layout.num_ctus(w, h))
+        assert np.array_equal(dec["best_mode"][f], bm) and np.array_equal(dec["best_cost"][f], bc), f
+
+
 def test_decisions_only_full_size_matches_table_argmin(gpu_available):
     """1080p (the bench size), 2 frames: the fused decisions-only search gives exactly the
     decision lists of the full cost table (best_mode_kernel over it)."""
