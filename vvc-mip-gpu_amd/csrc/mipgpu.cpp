@@ -965,18 +965,21 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
       HIP_TRY(to_dev(e->d_refs + fo * fs, refs_or_null + f0 * fs, nb * fs * 2, pin_in));
       d_refs = e->d_refs + fo * fs;
     }
+    // the engine filter runs on the upload stream behind the chunk's upload: it overlaps the
+    // previous chunk's search (its workgroups take CUs as the persistent search grid drains)
+    // and the slot's refs region is free once the slot's previous search is (waited above)
+    const bool filt = !refs_or_null && e->opts.filter != MIP_FILTER_NONE;
+    if (filt) {
+      if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][2], up));
+      if (mip_filter_device(d_frames, e->d_refs + fo * fs, e->width, e->height, nb, e->opts.filter,
+                            e->opts.kernel_idx, up) != 0)
+        return -1;
+      if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][3], up));
+      d_refs = e->d_refs + fo * fs;
+    }
     HIP_TRY(hipEventRecord(e->slot_up[sl], up));
     HIP_TRY(hipStreamWaitEvent(comp, e->slot_up[sl], 0));
     if (reuse) HIP_TRY(hipStreamWaitEvent(comp, e->slot_down[sl], 0));
-    const bool filt = !refs_or_null && e->opts.filter != MIP_FILTER_NONE;
-    if (filt) {
-      if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][2], comp));
-      if (mip_filter_device(d_frames, e->d_refs + fo * fs, e->width, e->height, nb, e->opts.filter,
-                            e->opts.kernel_idx, comp) != 0)
-        return -1;
-      if (e->trace) HIP_TRY(hipEventRecord(e->tr_ev[sl][3], comp));
-      d_refs = e->d_refs + fo * fs;
-    }
     if (e->trace) {
       e->tr_frames[sl] = nb;
       e->tr_filter[sl] = filt;
