@@ -832,8 +832,11 @@ __device__ __forceinline__ void walk_strip(const ORIG &orig, const RED &red, int
 
 // Paired walk (see PairAcc): the lane's blocks in [k0, k0 + windows) two at a time, rows
 // generated exactly as in walk_strip; block A's residual rows wait for block B's.
+#ifndef MIP_PAIR_MIN_AREA
+#define MIP_PAIR_MIN_AREA 32  // smallest CU area walked in block pairs (A/B knob; 33: 4x8 unpaired, -0.6 %)
+#endif
 template <int W, int H, int V>
-constexpr bool kPaired = Geo<W, H, V>::SID != 0 && W * H > 32 && V == kClassV[size_class(W, H)] &&
+constexpr bool kPaired = Geo<W, H, V>::SID != 0 && W * H >= MIP_PAIR_MIN_AREA && V == kClassV[size_class(W, H)] &&
                          ((Geo<W, H, V>::CHUNKED ? 4 * Geo<W, H, V>::UV : Geo<W, H, V>::KV * Geo<W, H, V>::UV) / 4) % 2 == 0;
 
 template <int W, int H, int V, class ORIG, class RED>
