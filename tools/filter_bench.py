@@ -13,18 +13,23 @@ import torch  # noqa: E402
 from mipgpu import FILTERS, filter_device  # noqa: E402
 from mipgpu.synth import synth_frames  # noqa: E402
 
-W, H, B, REPS = 1920, 1080, 32, 20
+W, H, REPS = 1920, 1080, 20
+B = int(os.environ.get("FB_FRAMES", 32))       # frames per launch
+KIDX = int(os.environ.get("FB_KIDX", 0))       # KernelIdx of every filter
+ONLY = os.environ.get("FB_ONLY")               # one filter name
 frames = torch.from_numpy(synth_frames(W, H, B, 0x1080, 0).astype(np.int16)).cuda()
 out = torch.empty_like(frames)
 s = torch.cuda.Stream()
 res = {}
 for name in FILTERS:
+    if ONLY and name != ONLY:
+        continue
     for _ in range(3):
-        filter_device(frames, out, name, 0, stream=s)
+        filter_device(frames, out, name, KIDX, stream=s)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(REPS):
-        filter_device(frames, out, name, 0, stream=s)
+        filter_device(frames, out, name, KIDX, stream=s)
     e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / REPS
@@ -44,5 +49,5 @@ e1.record(s)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / REPS
 copy = {"ms_per_launch": round(ms, 4), "GB/s": round(4 * W * H * B / (ms * 1e-3) / 1e9, 1)}
-print(json.dumps({"workload": "%dx%d x %d frames, kernel_idx 0" % (W, H, B), "filters": res,
+print(json.dumps({"workload": "%dx%d x %d frames, kernel_idx %d" % (W, H, B, KIDX), "filters": res,
                   "copy_calibration": copy}, indent=1))
