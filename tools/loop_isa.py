@@ -27,7 +27,7 @@ for i, l in enumerate(body):
     if m and m.group(1) in labels and labels[m.group(1)] < i:
         j = labels[m.group(1)]
         txt = "\n".join(body[j:i + 1])
-        if "v_mfma" in txt and "global_store" in txt and (best is None or i - j < best[2] - best[1]):
+        if "v_mfma" in txt and ("global_store" in txt or "buffer_store" in txt) and (best is None or i - j < best[2] - best[1]):
             best = (m.group(1), j, i + 1)
 lab, j, end = best
 seg = [x.strip().split(";")[0].strip() for x in body[j:end] if x.strip() and not x.strip().startswith((".", ";"))]

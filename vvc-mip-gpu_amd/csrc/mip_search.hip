@@ -971,6 +971,8 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
     cin = *reinterpret_cast<const f4 *>(ct + (m0 + (r & 1)) * G::NOUT + 4 * h);
   }
   constexpr int NCS = (G::SLOTS + 7) / 8;  // column sets (8 CUs x 2 modes) of a full task
+  // column sets holding CUs (scalar: the task's CU count is wave-uniform)
+  const int ncs_run = __builtin_amdgcn_readfirstlane((ncu + 7) >> 3);
   constexpr int NRB = G::CPOS / 16;        // 16-row blocks in this chunk
   // the lane's 4 results of block rb sit at stored positions pos0 + i * PSTEP
   // (padded rows: position (k, kx) at k*RP + kx + 1; outputs 4h..4h+3 share one row)
@@ -1006,7 +1008,7 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
     }
 #pragma unroll
     for (int cs = 0; cs < NCS; cs++) {
-      if (cs > 0 && 8 * cs >= ncu) break;  // wave-uniform: partial last task
+      if (cs > 0 && cs >= ncs_run) break;  // wave-uniform: partial last task
       const h4 bv = BATCH_B ? bvs[BATCH_B ? cs : 0] : *reinterpret_cast<const h4 *>(bbase + cs * 8 * kEntryBytes);
       const f4 d = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bv, cin, 0, 0, 0);
       // columns of slots >= ncu hold garbage; they land in unused scratch columns unless
@@ -1041,6 +1043,34 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
   if constexpr (N >= 64) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
   return v;
 }
+
+// A group sum's last DPP step must run before the store branch: only the storing lane uses
+// the sum, so the compiler sinks that add under the branch's exec mask, where the DPP read
+// cannot fold into it (v_mov_b32_dpp + v_add_u32 instead of one v_add_u32_dpp: 4 VALU per
+// mode pair in every class with more than one lane per CU).
+#ifndef MIP_PIN_SUMS
+#define MIP_PIN_SUMS 1  // A/B knob
+#endif
+__device__ __forceinline__ uint32_t pin_sum(uint32_t v) {
+#if MIP_PIN_SUMS
+  asm volatile("; pin" : "+v"(v));
+#endif
+  return v;
+}
+
+// Cost-table stores of a task: a buffer descriptor over the CTU's block (uniform per
+// item), the CU's byte offset as the per-lane VGPR offset (per task) and the mode pair's
+// offset as the scalar offset (per pair) -- the pair loop computes no per-lane address.
+struct CtuRows {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit CtuRows(int32_t *ctu_block) {
+    r = __builtin_amdgcn_make_buffer_rsrc(ctu_block, 0, MIP_COSTS_PER_CTU * 4, 0x00020000);
+  }
+  __device__ __forceinline__ void store(uint32_t cu_ofs, int mq, int v0, int v1) const {
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)v0, (unsigned)v1}, r, (int)cu_ofs, mq * 4, 0);
+  }
+};
 
 // Opaque copy of a value: keeps per-class lane arithmetic inside its switch case (hoisted
 // out of the task loop it would stay live through every class and spill).
@@ -1091,7 +1121,10 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_ti
   }
   std::conditional_t<TR, OrigRowsT<H>, OrigRows<H>> orig;
   orig.load(x.org, c.lx + x0, c.ly);
-  const size_t cbase = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU + job.cost;
+  const size_t ctu_row = ((size_t)x.frame * a.nctus + x.ctu) * MIP_COSTS_PER_CTU;  // uniform
+  const uint32_t cu_ofs = (uint32_t)job.cost * 4;                                  // < 2^19 bytes
+  const CtuRows rows_cost(a.cost ? a.cost + ctu_row : nullptr), rows_sad(a.sad ? a.sad + ctu_row : nullptr),
+      rows_satd(a.satd ? a.satd + ctu_row : nullptr);  // optional tables: null (never stored to)
   const uint32_t *mine = reinterpret_cast<const uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
   const Red<G::R, G::RP> red{mine, 0};
   s2 top[4];  // top boundary of the strip: upsampling state above window 0
@@ -1158,38 +1191,38 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_ti
     uint32_t sad0, sad1, satd0, satd1;
     int c0, c1;  // min(2 * SAD, SATD) of the pair's modes (intra.cl:1166)
     if constexpr (PAIRED) {
-      sad0 = group_sum<GS>(acc.sad0);
-      sad1 = group_sum<GS>(acc.sad1);
-      satd0 = group_sum<GS>(acc.t0) >> 1;
-      satd1 = group_sum<GS>(acc.t1) >> 1;
+      sad0 = pin_sum(group_sum<GS>(acc.sad0));
+      sad1 = pin_sum(group_sum<GS>(acc.sad1));
+      satd0 = pin_sum(group_sum<GS>(acc.t0)) >> 1;
+      satd1 = pin_sum(group_sum<GS>(acc.t1)) >> 1;
       c0 = min(2 * (int)sad0, (int)satd0);
       c1 = min(2 * (int)sad1, (int)satd1);
     } else if constexpr (W * H <= 32) {
-      const uint32_t sp = group_sum<GS>(acc.sad), tp = group_sum<GS>(acc.satd);
+      const uint32_t sp = pin_sum(group_sum<GS>(acc.sad)), tp = pin_sum(group_sum<GS>(acc.satd));
       const uint32_t cp = as_u32(__builtin_elementwise_min(as_u2(sp) << (u2){1, 1}, as_u2(tp)));
       c0 = (int)(cp & 0xffff);
       c1 = (int)(cp >> 16);
       sad0 = sp & 0xffff, sad1 = sp >> 16, satd0 = tp & 0xffff, satd1 = tp >> 16;
     } else {
       acc.flush();
-      sad0 = group_sum<GS>(acc.sad0);
-      sad1 = group_sum<GS>(acc.sad1);
-      satd0 = group_sum<GS>(acc.satd0);
-      satd1 = group_sum<GS>(acc.satd1);
+      sad0 = pin_sum(group_sum<GS>(acc.sad0));
+      sad1 = pin_sum(group_sum<GS>(acc.sad1));
+      satd0 = pin_sum(group_sum<GS>(acc.satd0));
+      satd1 = pin_sum(group_sum<GS>(acc.satd1));
       c0 = min(2 * (int)sad0, (int)satd0);
       c1 = min(2 * (int)sad1, (int)satd1);
     }
     if (active && sub == GS - 1) {
       // the CU's modes of view pair q (TR: the other orientation)
       const int mq = TR ? (2 * q < G::MODES ? 2 * q + G::MODES : 2 * q - G::MODES) : 2 * q;
-      const size_t idx = cbase + mq;  // every CU of a task lies inside the frame (build_work)
       if constexpr (DEC) {
         // costs < 2^23 (256 blocks x 32736): the packed order is cost, then the lower mode
         best = min(best, min((uint32_t)c0 << 5 | (uint32_t)mq, (uint32_t)c1 << 5 | (uint32_t)(mq + 1)));
       } else {
-        *reinterpret_cast<int2 *>(a.cost + idx) = make_int2(c0, c1);
-        if (a.sad) *reinterpret_cast<int2 *>(a.sad + idx) = make_int2(sad0, sad1);
-        if (a.satd) *reinterpret_cast<int2 *>(a.satd + idx) = make_int2(satd0, satd1);
+        // every CU of a task lies inside the frame (build_work)
+        rows_cost.store(cu_ofs, mq, c0, c1);
+        if (a.sad) rows_sad.store(cu_ofs, mq, (int)sad0, (int)sad1);
+        if (a.satd) rows_satd.store(cu_ofs, mq, (int)satd0, (int)satd1);
       }
     }
   }
