@@ -685,20 +685,20 @@ struct OrigRows {
   using Block = BlockAcc;
   static constexpr bool CACHED = H <= 4;
   uint2 r[CACHED ? H : 1];
-  const uint16_t *tile;
-  int x, y;
+  const uint16_t *row0;  // the strip's first sample (row y, column x)
   __device__ __forceinline__ void load(const uint16_t *t, int xx, int yy) {
-    tile = t;
-    x = xx;
-    y = yy;
+    row0 = t + tidx(xx, yy);
     if constexpr (CACHED) {
 #pragma unroll
       for (int i = 0; i < H; i++) r[i] = lds_row4(t, xx, yy + i);
     }
   }
+  // Row i as a constant stride from row0: a runtime block-pair base (walk_pairs' yb) plus a
+  // constant row becomes one address per block pair and immediate offsets (through tidx the
+  // compiler emitted an add and a v_mad_u32_u24 per row read).
   __device__ __forceinline__ uint2 operator()(int i) const {
     if constexpr (CACHED) return r[i];
-    else return lds_row4(tile, x, y + i);
+    else return *reinterpret_cast<const uint2 *>(row0 + i * kPitch);
   }
 };
 
@@ -846,7 +846,9 @@ __device__ __forceinline__ void walk_pairs(const ORIG &orig, const RED &red, int
   constexpr int ROWS = G::CHUNKED ? 4 * G::UV : G::KV * G::UV;  // CU rows of this call
   constexpr int NBP = ROWS / 8;                                   // block pairs
   const int y0 = k0 * G::UV;                                      // first CU row
-  // per block pair: 4 rows of A -> dA, 4 rows of B -> pair_row
+  // per block pair: 4 rows of A -> dA, 4 rows of B -> pair_row.  (Unrolling two block pairs,
+  // which drops the loop-carried copies of the top boundary and the zeroed accumulators --
+  // 8 v_mov per pair -- measured flat: 7544 -> 7532 frames/s, and spills in the ALT kernels.)
 #pragma unroll 1
   for (int bp = 0; bp < NBP; bp++) {
     uint32_t dA[16], t0[16], t1[16];
