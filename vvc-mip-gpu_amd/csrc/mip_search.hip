@@ -1249,9 +1249,6 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_ti
 // (deterministic) costs.  Indexes past the frame's end and the columns left of a frame's
 // first column read as 0 (+ bias): they only feed CUs whose costs the reference leaves
 // undefined (no task) or padding branches that never select them.
-constexpr int kTileChunks = kPitch / 4;            // 17 chunks of 4 samples per row
-constexpr int kTileLoads = 65 * kTileChunks;       // 1105 8-byte chunks per quadrant window
-
 // 8-byte chunk at linear index fy * width + fx (fx % 4 == 0, width % 4 == 0: a chunk lies
 // entirely inside or entirely outside [0, width * height)).
 __device__ __forceinline__ uint2 frame_chunk(const uint16_t *frame, int width, int height, int fx, int fy) {
@@ -1261,31 +1258,83 @@ __device__ __forceinline__ uint2 frame_chunk(const uint16_t *frame, int width, i
   return v;
 }
 
-__device__ __forceinline__ uint2 tile_load(const uint16_t *frame, int width, int height, int x0, int y0, int i) {
-  const int row = i / kTileChunks, ch = i - row * kTileChunks;
-  return frame_chunk(frame, width, height, x0 - kColOff + 4 * ch, y0 - 1 + row);
-}
-
-__device__ __forceinline__ void tile_store(uint16_t *dst, int i, uint2 v) {
-  const int row = i / kTileChunks, ch = i - row * kTileChunks;
-  // residual bias of the sample's 4x4-block position (quadrant y = row - 1, x = 4ch - 4)
-  const uint32_t odd = (row - 1) & 1;
-  v.x += odd ? bias_word(1, 0) : bias_word(0, 0);
-  v.y += odd ? bias_word(1, 2) : bias_word(0, 2);
-  *reinterpret_cast<uint2 *>(dst + row * kPitch + 4 * ch) = v;
-}
+// Window staging by a group of P threads (P = 64: the prefetching wave; 512: the workgroup).
+// Thread p takes the main chunk column 1 + (p & 15) (quadrant columns 4 (p & 15) .. +3) of
+// window rows p / 16 + (P / 16) k, and the left halo chunk (columns -4..-1) of rows p + P k.
+// Everything per thread but the row step is fixed per item, so a chunk costs one address
+// add and the two bias adds: the loads go through a buffer descriptor over the frame, whose
+// range check reads indexes past the frame's end as 0 (frame_chunk's `li < W * H`; a chunk
+// lies entirely inside or outside, W % 4 == 0), the row above the frame and the columns left
+// of it are forced out of range (uniform tests), and the LDS offsets are immediates.  (The
+// chunk-index form, row = i / 17 per chunk, cost ~20 VALU per chunk: ~0.9 % of the kernel.)
+template <int P>
+struct WindowStager {
+  static constexpr int RIT = P / 16;                 // window rows per main round
+  static constexpr int NMAIN = (65 + RIT - 1) / RIT;  // main rounds
+  static constexpr int NHALO = (65 + P - 1) / P;      // halo rounds
+  static constexpr int N = NMAIN + NHALO;
+  static constexpr uint32_t kOut = 0x80000000u;       // an out-of-range byte offset
+  __amdgpu_buffer_rsrc_t rsrc;
+  int p, vmain, vhalo, W2;  // thread, byte offsets of its main / halo chunk in round 0, row bytes
+  bool top, left;           // the window's row -1 / columns -4..-1 lie outside the frame
+  uint32_t bmx, bmy, bhx, bhy;  // residual biases of its main / halo rows (kBiasD)
+  __device__ __forceinline__ WindowStager(const uint16_t *frame, int width, int height, int fx0, int fy0, int thread) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(frame), 0, width * height * 2, 0x00020000);
+    p = thread;
+    W2 = width * 2;
+    top = fy0 == 0;
+    left = fx0 == 0;
+    vmain = ((fy0 - 1 + p / 16) * width + fx0 + 4 * (p & 15)) * 2;
+    vhalo = ((fy0 - 1 + p) * width + fx0 - 4) * 2;
+    const bool om = ((p / 16 - 1) & 1) != 0, oh = ((p - 1) & 1) != 0;  // row parity (RIT, P even)
+    bmx = om ? bias_word(1, 0) : bias_word(0, 0);
+    bmy = om ? bias_word(1, 2) : bias_word(0, 2);
+    bhx = oh ? bias_word(1, 0) : bias_word(0, 0);
+    bhy = oh ? bias_word(1, 2) : bias_word(0, 2);
+  }
+  __device__ __forceinline__ bool valid(int k) const {
+    return k < NMAIN ? (k < NMAIN - 1 || p / 16 + RIT * k < 65) : p + P * (k - NMAIN) < 65;
+  }
+  __device__ __forceinline__ uint2 load(int k) const {
+    uint32_t o;
+    if (k < NMAIN) {
+      o = vmain + k * RIT * W2;
+      if (k == 0 && top) o = p < 16 ? kOut : o;  // row -1 above the frame
+    } else {
+      o = vhalo + (k - NMAIN) * P * W2;
+      if (left) o = kOut;                         // columns left of the frame
+      if (k == NMAIN && top) o = p == 0 ? kOut : o;
+    }
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)o, 0, 0);
+    return make_uint2(v.x, v.y);
+  }
+  __device__ __forceinline__ void store(uint16_t *dst, int k, uint2 v) const {
+    if (k < NMAIN) {
+      v.x += bmx;
+      v.y += bmy;
+      *reinterpret_cast<uint2 *>(dst + (p / 16 + RIT * k) * kPitch + 4 + 4 * (p & 15)) = v;
+    } else {
+      v.x += bhx;
+      v.y += bhy;
+      *reinterpret_cast<uint2 *>(dst + (p + P * (k - NMAIN)) * kPitch) = v;
+    }
+  }
+};
 
 // (whole workgroup, kWaves * 64 threads: every thread's loads are issued before its first
-// LDS store, so the workgroup waits for HBM once, not once per load; spare threads of the
-// last round repeat the last chunk -- same value, same LDS slot)
+// LDS store, so the workgroup waits for HBM once, not once per load)
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
                                            int x0, int y0) {
-  constexpr int NT = 64 * kWaves, NL = (kTileLoads + NT - 1) / NT;
-  uint2 v[NL];
+  const WindowStager<64 * kWaves> st(frame, width, height, x0, y0, (int)threadIdx.x);
+  constexpr int N = WindowStager<64 * kWaves>::N;
+  uint2 v[N];
 #pragma unroll
-  for (int k = 0; k < NL; k++) v[k] = tile_load(frame, width, height, x0, y0, min((int)threadIdx.x + NT * k, kTileLoads - 1));
+  for (int k = 0; k < N; k++)
+    if (st.valid(k)) v[k] = st.load(k);
 #pragma unroll
-  for (int k = 0; k < NL; k++) tile_store(dst, min((int)threadIdx.x + NT * k, kTileLoads - 1), v[k]);
+  for (int k = 0; k < N; k++)
+    if (st.valid(k)) st.store(dst, k, v[k]);
 }
 
 // Item = (frame, CTU, quadrant, slice) -> quadrant origin in the frame and frame index.
@@ -1529,20 +1578,17 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
           const uint16_t *nframe = a.orig + (size_t)np.frame * a.width * a.height;
           uint16_t *dst = org_buf + (par ^ 1) * kTileElems;
           // loads in flight MIP_PF_BATCH at a time, then their stores
-          constexpr int NL = (kTileLoads + 63) / 64, NB = MIP_PF_BATCH;
-#pragma unroll 1
+          const WindowStager<64> st(nframe, a.width, a.height, np.fx0, np.fy0, lane);
+          constexpr int NL = WindowStager<64>::N, NB = MIP_PF_BATCH;
+#pragma unroll
           for (int k0 = 0; k0 < NL; k0 += NB) {
             uint2 v[NB];
 #pragma unroll
-            for (int k = 0; k < NB; k++) {
-              const int i = lane + 64 * (k0 + k);
-              v[k] = i < kTileLoads ? tile_load(nframe, a.width, a.height, np.fx0, np.fy0, i) : make_uint2(0, 0);
-            }
+            for (int k = 0; k < NB; k++)
+              if (k0 + k < NL && st.valid(k0 + k)) v[k] = st.load(k0 + k);
 #pragma unroll
-            for (int k = 0; k < NB; k++) {
-              const int i = lane + 64 * (k0 + k);
-              if (i < kTileLoads) tile_store(dst, i, v[k]);
-            }
+            for (int k = 0; k < NB; k++)
+              if (k0 + k < NL && st.valid(k0 + k)) st.store(dst, k0 + k, v[k]);
           }
         }
         if (lane == 0) {
