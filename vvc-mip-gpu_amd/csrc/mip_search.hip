@@ -1275,17 +1275,20 @@ struct WindowStager {
   static constexpr int N = NMAIN + NHALO;
   static constexpr uint32_t kOut = 0x80000000u;       // an out-of-range byte offset
   __amdgpu_buffer_rsrc_t rsrc;
-  int p, vmain, vhalo, W2;  // thread, byte offsets of its main / halo chunk in round 0, row bytes
+  int p;                    // thread
+  uint32_t vmain, vhalo, W2;  // byte offsets of its main / halo chunk in round 0 (mod 2^32), row bytes
   bool top, left;           // the window's row -1 / columns -4..-1 lie outside the frame
   uint32_t bmx, bmy, bhx, bhy;  // residual biases of its main / halo rows (kBiasD)
   __device__ __forceinline__ WindowStager(const uint16_t *frame, int width, int height, int fx0, int fy0, int thread) {
-    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(frame), 0, width * height * 2, 0x00020000);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(frame), 0, (int)((uint32_t)width * height * 2u), 0x00020000);
     p = thread;
-    W2 = width * 2;
+    W2 = (uint32_t)width * 2;
     top = fy0 == 0;
     left = fx0 == 0;
-    vmain = ((fy0 - 1 + p / 16) * width + fx0 + 4 * (p & 15)) * 2;
-    vhalo = ((fy0 - 1 + p) * width + fx0 - 4) * 2;
+    // (fy0 + 64) * width < 2^31 (mip_engine_create); the byte offsets wrap like the range
+    // check's unsigned compare expects (row -1 above the frame is forced out of range anyway)
+    vmain = (uint32_t)((fy0 - 1 + p / 16) * width + fx0 + 4 * (p & 15)) * 2u;
+    vhalo = (uint32_t)((fy0 - 1 + p) * width + fx0 - 4) * 2u;
     const bool om = ((p / 16 - 1) & 1) != 0, oh = ((p - 1) & 1) != 0;  // row parity (RIT, P even)
     bmx = om ? bias_word(1, 0) : bias_word(0, 0);
     bmy = om ? bias_word(1, 2) : bias_word(0, 2);
@@ -1298,10 +1301,10 @@ struct WindowStager {
   __device__ __forceinline__ uint2 load(int k) const {
     uint32_t o;
     if (k < NMAIN) {
-      o = vmain + k * RIT * W2;
+      o = vmain + (uint32_t)(k * RIT) * W2;
       if (k == 0 && top) o = p < 16 ? kOut : o;  // row -1 above the frame
     } else {
-      o = vhalo + (k - NMAIN) * P * W2;
+      o = vhalo + (uint32_t)((k - NMAIN) * P) * W2;
       if (left) o = kOut;                         // columns left of the frame
       if (k == NMAIN && top) o = p == 0 ? kOut : o;
     }
