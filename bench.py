@@ -138,13 +138,31 @@ def algorithmic_bytes_per_frame(w, h):
     return w * h * 2 + num_ctus(w, h) * COSTS_PER_CTU * 4
 
 
-def load_pmc(width, height, frames):
-    """PMC summary (tools/pmc_profile.sh + tools/traffic_json.py) for this workload, or {}."""
+def load_pmc(width, height, frames, build):
+    """PMC summary (tools/profile_round.sh -> tools/traffic_json.py) for this workload, or {}.
+    Only a profile of THIS build counts: the entry's build ID must name the same sources and
+    flags as the loaded library (mip_build_id), else the PMC fields are left null."""
+    from mipgpu import source_id
     path = os.path.join(REPO, "profiles", "traffic.json")
     try:
-        return json.load(open(path)).get("%dx%dx%d" % (width, height, frames), {})
+        rec = json.load(open(path)).get("%dx%dx%d" % (width, height, frames), {})
     except Exception:
-        return {}
+        return {}, "no profiles/traffic.json entry for this workload"
+    if not rec:
+        return {}, "no profiles/traffic.json entry for this workload"
+    if source_id(rec.get("build_id", "")) != source_id(build):
+        return {}, "profiles/traffic.json was collected on build %r, not this one" % rec.get("build_id")
+    return rec, "profiles/traffic.json, same build"
+
+
+# Environment knobs of libmipgpu.so that change the work or the launch shape (profiling / A/B
+# tools).  A headline number is refused while any of them is set; --allow-knobs (the A/B
+# scripts) records them in the line instead.  Print-only diagnostics are harmless.
+HARMLESS_KNOBS = {"MIPGPU_STAGE_STATS", "MIPGPU_WORK_STATS"}
+
+
+def active_knobs():
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("MIPGPU_") and k not in HARMLESS_KNOBS}
 
 
 def valu_section(pmc, kernel_ms, alg_ops):
@@ -239,7 +257,13 @@ def reference_gpu(width, height, frames, seed):
         d = json.loads(out.strip().splitlines()[-1])
         if not d["device_ms_per_frame"] > 0:
             return {"error": "no device timing", "raw": d}
-        return {"value": round(1000.0 / d["device_ms_per_frame"], 3), "unit": "frames/s (device time)",
+        # device time from the CL profiling timestamps of every kernel; a kernel whose
+        # timestamps are unusable is timed by the host around enqueue + clFinish instead, and
+        # then the figure is labelled as such
+        fb = int(d.get("event_fallbacks", 0))
+        unit = "frames/s (device time, CL profiling events)" if fb == 0 else \
+            "frames/s (host wall time around each kernel: %d CL profiling events unusable)" % fb
+        return {"value": round(1000.0 / d["device_ms_per_frame"], 3), "unit": unit, "event_fallbacks": fb,
                 "wall_value": round(1000.0 / d["wall_ms_per_frame"], 2),
                 "kernel_ms_per_frame": d["kernel_ms"], "device": d["device"],
                 "note": "reference intra.cl kernels (initBoundaries, MIP_ReducedPred, 3x upsampleDistortion) "
@@ -248,15 +272,16 @@ def reference_gpu(width, height, frames, seed):
         return {"error": str(exc)[:200]}
 
 
-def ranks_section(per_rank, frames_per_step, steps, backend):
+def ranks_section(per_rank, frames_per_step, steps, backend, devices=None):
     """Rank count actually running (dist.get_world_size()) and each rank's own rate (its own
     search launches' device time: the wall time between the barriers is the slowest rank's
-    for every rank)."""
+    for every rank).  devices: GPUs visible to a rank (ranks share a GPU when world > devices)."""
     world = len(per_rank)
     if world > 1:
         import torch.distributed as dist
         world = dist.get_world_size()
-    return {"world_size": world, "backend": backend,
+    return {"world_size": world, "backend": backend, "devices": devices,
+            "shared_devices": bool(devices) and world > devices,
             "per_rank_frames_per_s": [round(frames_per_step / (r[1] * 1e-3), 2) for r in per_rank],
             "per_rank_kernel_ms": [round(r[1], 4) for r in per_rank]}
 
@@ -308,11 +333,19 @@ def main():
                     help="alternative references: run this reference filter (e.g. filterFrame_2d_int_quarterCtu) "
                          "inside every step (BASELINE configs[2]/[4]); default: original references")
     ap.add_argument("--kernel-idx", type=int, default=0, help="KernelIdx of --refs-filter")
+    ap.add_argument("--allow-knobs", action="store_true",
+                    help="A/B tooling only: run although MIPGPU_* work knobs are set (they are recorded in the "
+                         "line, which is then marked as no headline)")
     ap.add_argument("--plumbing-check", action="store_true",
                     help="CPU only (gloo): run the rank launch, timing reduction and JSON line with a "
                          "sleep in place of the search (tests/test_bench_dist.py)")
     args = ap.parse_args()
 
+    knobs = active_knobs()
+    if knobs and not args.allow_knobs:
+        print("bench.py: refusing to measure with libmipgpu work knobs set (%s): they change the work or the "
+              "launch shape; unset them (A/B tools pass --allow-knobs)" % ", ".join(knobs), file=sys.stderr)
+        sys.exit(3)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
@@ -330,16 +363,26 @@ def main():
     from mipgpu.synth import synth_frames_torch
 
     rank, local_rank, world = dist_env()
+    # One rank per GPU; more ranks than GPUs (a rehearsal of the N-GPU path on a smaller box)
+    # put rank r on device r % count and carry the barriers / timing reductions over gloo
+    # (RCCL needs a device per rank).  Frames stay sharded per rank either way.
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % max(1, ndev)
+    backend = "nccl" if world <= ndev else "gloo"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = None if backend == "gloo" else torch.device("cuda", dev_index)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     W, H, B = args.width, args.height, args.frames_per_step
 
     # synthetic frames generated on the GPU (bit-identical to mipgpu.synth.synth_frames)
     frames = synth_frames_torch(W, H, B, shard_seed(args.seed, rank), 0, device=dev)
-    eng = MipEngine(W, H, device=local_rank, max_batch=B, slices_per_ctu=args.slices, filter=args.refs_filter,
+    eng = MipEngine(W, H, device=dev_index, max_batch=B, slices_per_ctu=args.slices, filter=args.refs_filter,
                     kernel_idx=args.kernel_idx)
     costs = torch.empty((B, eng.costs_per_frame), dtype=torch.int32, device=dev)
     stream = torch.cuda.Stream(dev)  # the search kernels and the timing events share it
@@ -363,7 +406,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one search launch per step, same stream
 
-    per_rank = gather_ranks([elapsed, kernel_ms], world, dev)
+    per_rank = gather_ranks([elapsed, kernel_ms], world, coll_dev)
     max_elapsed = max(r[0] for r in per_rank)
     max_kernel_ms = max(r[1] for r in per_rank)
     value, ms_per_step = aggregate(B, args.steps, world, max_elapsed)
@@ -378,7 +421,9 @@ def main():
         alg_bytes = algorithmic_bytes_per_frame(W, H) * B
         achieved = alg_bytes / (max_kernel_ms * 1e-3) / 1e9
         ops = VECTOR_OPS_PER_CTU * num_ctus(W, H) * B
-        pmc = load_pmc(W, H, B)
+        from mipgpu import build_id
+        build = build_id()
+        pmc, pmc_src = load_pmc(W, H, B, build)
         res = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -394,8 +439,13 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes},
             # The bound that applies: VALU issue (see the module docstring).
             "valu": valu_section(pmc, max_kernel_ms, ops),
-            "ranks": ranks_section(per_rank, B, args.steps, "nccl" if world > 1 else None),
+            "ranks": ranks_section(per_rank, B, args.steps, backend if world > 1 else None,
+                                   devices=ndev),
+            "build_id": build, "pmc_source": pmc_src,
         }
+        if knobs:
+            res["knobs"] = knobs
+            res["headline"] = False  # measured with work knobs set (A/B tooling)
         if world == 1 and not args.no_filter:
             res["filter"] = filter_section(MipEngine, frames, W, H, B, stream, dev, 5, pmc)
         if world == 1 and not args.no_latency:

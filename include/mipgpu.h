@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MIPGPU_ABI_VERSION 5
+#define MIPGPU_ABI_VERSION 6
 #define MIP_COSTS_PER_CTU_ABI 97840
 #define MIP_CUS_PER_CTU_ABI 5380
 #define MIP_COST_UNAVAILABLE 0x7fffffff
@@ -190,6 +190,9 @@ int mip_host_free(void *p);
 /* Last error message of the calling thread ("" if none). */
 const char *mip_last_error(void);
 int mip_abi_version(void);
+/* Build ID of this library: "src:<hash of the sources and compiler flags> git:<commit>"
+ * (+ "knobs:<-D options>" for A/B variants).  bench.py prints it and ties profiles/ to it. */
+const char *mip_build_id(void);
 
 #ifdef __cplusplus
 }

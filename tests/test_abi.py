@@ -39,7 +39,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_geometry_helpers(lib):
-    assert lib.mip_abi_version() == 5
+    assert lib.mip_abi_version() == 6
     assert lib.mip_num_ctus(1920, 1080) == 135
     assert lib.mip_num_ctus(3840, 2160) == 510
     assert lib.mip_num_ctus(7680, 4320) == 2040
@@ -100,3 +100,12 @@ def test_engine_create_rejects_bad_arguments_before_touching_the_gpu(lib):
     assert 195 * 2040 * 5380 <= (1 << 31) - 256 < 196 * 2040 * 5380
     with pytest.raises(mipgpu.MipError, match="CUs per launch"):
         mipgpu.MipEngine(7680, 4320, max_batch=196)
+
+
+def test_build_id_names_the_sources(lib):
+    """mip_build_id(): the hash of the sources + flags the library was built from (the Makefile
+    computes it the same way), so a bench line / profile can be tied to its build."""
+    bid = mipgpu.build_id()
+    assert bid.startswith("src:") and " git:" in bid, bid
+    want = subprocess.check_output(["make", "-s", "-C", os.path.join(REPO, "vvc-mip-gpu_amd"), "build-id"]).decode()
+    assert mipgpu.source_id(bid) == mipgpu.source_id(want.strip())

@@ -81,3 +81,42 @@ def test_gpus_flag_must_match_launcher():
     r = subprocess.run([sys.executable, bench.__file__, "--gpus", "4", "--plumbing-check"], capture_output=True,
                        text=True, timeout=120, env=env)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_work_knobs_are_refused():
+    """A headline number is never measured with a work-changing library knob set
+    (MIPGPU_NO_PAIRS searches no mode pair, MIPGPU_SHAPE_FILTER drops shapes, ...): exit 3
+    before anything runs; --allow-knobs (A/B tools) lets the run go on and records them."""
+    import json
+    import subprocess
+    import sys
+    base = {k: v for k, v in os.environ.items() if not k.startswith("MIPGPU_")
+            and k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    for knob in ("MIPGPU_NO_PAIRS", "MIPGPU_SHAPE_FILTER", "MIPGPU_GROUPS", "MIPGPU_LIB"):
+        r = subprocess.run([sys.executable, bench.__file__, "--plumbing-check", "--steps", "1"], capture_output=True,
+                           text=True, timeout=120, env=dict(base, **{knob: "1"}))
+        assert r.returncode == 3 and knob in r.stderr, (knob, r.returncode, r.stderr)
+    r = subprocess.run([sys.executable, bench.__file__, "--plumbing-check", "--steps", "1", "--allow-knobs"],
+                       capture_output=True, text=True, timeout=120, env=dict(base, MIPGPU_NO_PAIRS="1"))
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+    # print-only diagnostics do not count
+    r = subprocess.run([sys.executable, bench.__file__, "--plumbing-check", "--steps", "1"], capture_output=True,
+                       text=True, timeout=120, env=dict(base, MIPGPU_STAGE_STATS="1"))
+    assert r.returncode == 0, r.stderr
+
+
+def test_pmc_profile_of_another_build_is_not_used(tmp_path, monkeypatch):
+    """bench.load_pmc takes profiles/traffic.json's numbers only when the entry's build ID
+    names the same sources and flags as the loaded library."""
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "traffic.json").write_text(json.dumps({"64x64x2": {"build_id": "src:aaaa git:x", "hbm_bytes_per_launch": 5}}))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    rec, why = bench.load_pmc(64, 64, 2, "src:aaaa git:y")
+    assert rec["hbm_bytes_per_launch"] == 5 and "same build" in why
+    rec, why = bench.load_pmc(64, 64, 2, "src:bbbb git:x")
+    assert rec == {} and "src:aaaa" in why
+    rec, why = bench.load_pmc(64, 64, 3, "src:aaaa git:x")
+    assert rec == {}

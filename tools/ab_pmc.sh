@@ -10,7 +10,7 @@ COUNTERS=${COUNTERS:-"SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_
 for lib in "$@"; do
   name=$(basename "$lib" .so)
   MIPGPU_LIB=$PWD/$lib timeout -s KILL 120 rocprofv3 --pmc $COUNTERS -d "$OUT/$name" -o pmc --output-format csv -- \
-    python bench.py --frames-per-step 32 --steps 3 --warmup 1 --no-cpu-baseline --no-reference-gpu --no-latency \
+    python bench.py --frames-per-step 32 --steps 3 --warmup 1 --allow-knobs --no-cpu-baseline --no-reference-gpu --no-latency \
     --no-end-to-end --no-filter > "$OUT/$name.log" 2>&1 || { tail -20 "$OUT/$name.log"; exit 1; }
   python3 - "$OUT/$name" "$name" <<'PY'
 import csv, glob, sys, collections

@@ -19,6 +19,7 @@ echo "== kernel trace $(date +%T)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$RAW/trace" -o run --output-format csv -- \
   python3 bench.py --steps 10 $ARGS > "$OUT/trace_bench.json" 2> "$RAW/trace.err" || { tail -20 "$RAW/trace.err"; exit 1; }
 find "$RAW/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
+python3 -c "import sys; sys.path.insert(0, 'vvc-mip-gpu_amd'); import mipgpu; print(mipgpu.build_id())" > "$OUT/build_id.txt"
 head -5 "$OUT/kernel_stats.csv"
 i=0
 while read -r counters; do

@@ -73,6 +73,10 @@ f = traffic(collect(FILTER))
 if f:
     f["kernel"] = FILTER
     rec["filter"] = f
+# the library build the passes profiled (bench.py accepts PMC data only from the same build)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vvc-mip-gpu_amd"))
+import mipgpu  # noqa: E402
+rec["build_id"] = mipgpu.build_id()
 d = json.load(open(out)) if os.path.exists(out) else {}
 d[key] = rec
 json.dump(d, open(out, "w"), indent=1)

@@ -476,6 +476,10 @@ void mip_opts_default(mip_opts *o) {
 
 const char *mip_last_error(void) { return g_err.c_str(); }
 int mip_abi_version(void) { return MIPGPU_ABI_VERSION; }
+#ifndef MIPGPU_BUILD_ID
+#define MIPGPU_BUILD_ID "src:unversioned"
+#endif
+const char *mip_build_id(void) { return MIPGPU_BUILD_ID; }
 
 int mip_num_ctus(int width, int height) { return ((width + 127) / 128) * ((height + 127) / 128); }
 int64_t mip_costs_per_frame(int width, int height) { return (int64_t)mip_num_ctus(width, height) * MIP_COSTS_PER_CTU; }

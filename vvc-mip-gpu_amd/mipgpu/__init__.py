@@ -93,6 +93,7 @@ def library():
         "mip_host_free": (ip, [vp]),
         "mip_last_error": (ctypes.c_char_p, []),
         "mip_abi_version": (ip, []),
+        "mip_build_id": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -100,6 +101,16 @@ def library():
         fn.argtypes = args
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """mip_build_id(): 'src:<source + flag hash> git:<commit>[ knobs:...]'."""
+    return library().mip_build_id().decode()
+
+
+def source_id(bid: str) -> str:
+    """The part of a build ID that identifies the compiled code (the 'src:' token)."""
+    return bid.split()[0] if bid else ""
 
 
 def _check(rc):
@@ -316,6 +327,6 @@ def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
     return frames_out
 
 
-__all__ = ["MipEngine", "MipError", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "topk_device", "library",
+__all__ = ["MipEngine", "MipError", "build_id", "source_id", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "topk_device", "library",
            "pinned_empty",
            "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]
