@@ -16,6 +16,13 @@
  * an engine must be used by one host thread at a time.  Samples are 10-bit values in
  * uint16; frames are row-major, consecutive frames are concatenated.
  *
+ * Input contract: every sample of a frame (and of caller-supplied reference frames) is at
+ * most 1023, like the reference's 10-bit constants (valueDC 512, clip 1023,
+ * constants.cl:22-23).  The search kernel detects a staged sample above 1023 and the engine
+ * reports it as an error (costs of such a frame are not valid): mip_search_frames /
+ * mip_wait fail for the call that searched it; device-API searches are asynchronous, so
+ * their violation is reported by mip_check_input or by the engine's next search call.
+ *
  * Cost layout (identical to the reference's ALL_stridedDistortionsPerCtu,
  * constants.h:1558-1631): int32 [frames][nCTUs][97840], entry
  *     ctu*97840 + shape_offset + cu*2*modes + mode
@@ -136,6 +143,11 @@ int mip_wait(mip_engine *e, uint64_t ticket);
 int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs,
                       int nframes, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
                       uint8_t *d_best_mode, int32_t *d_best_cost, void *stream);
+
+/* Input-contract check of the device-API searches issued on `stream` (a hipStream_t, NULL =
+ * the null stream): synchronises the stream, returns <0 (mip_last_error names it) if a
+ * search of this engine staged a sample above 1023 since the last check, else 0. */
+int mip_check_input(mip_engine *e, void *stream);
 
 /* mip_search_device restricted to the CTUs [ctu_begin, ctu_end) (raster order) of every
  * frame: writes exactly those CTUs' blocks of the full-size cost / SAD / SATD tables and

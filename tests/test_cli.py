@@ -303,3 +303,20 @@ def test_best_modes_of_unlogged_frames(gpu_available, tmp_path):
         shapes = [s for s in layout.SHAPES for _ in range(s.ncu)] * n
         want = [(-1, -1) if m == 0xFF else (int(m) % s.modes, int(m >= s.modes)) for m, s in zip(bm, shapes)]
         assert [(int(x["BestMode"]), int(x["Transposed"])) for x in got] == want, f
+
+
+@pytest.mark.gpu
+@needs_cli
+def test_samples_above_10_bits_are_refused(gpu_available, tmp_path):
+    """Input contract (include/mipgpu.h): a 12-bit sample (4095) in the CSV stops the CLI with
+    exit 1 and its position; in a raw input (no CPU check) the engine's kernel-side check fails
+    the search: exit 1, no log of wrong costs."""
+    W, H, N = 128, 128, 2
+    frames = synth_frames(W, H, N, 0xC17, 0)
+    frames[1, 37, 101] = 4095
+    write_csv(tmp_path / "in.csv", frames)
+    r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / "in.csv"), "-l", str(tmp_path / "o")])
+    assert r.returncode == 1 and "1:37:101 (frame:row:column) is above 10 bits" in r.stdout, r.stdout + r.stderr
+    frames.astype("<u2").tofile(tmp_path / "in.u16")
+    r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / "in.u16"), "-l", str(tmp_path / "o2")])
+    assert r.returncode == 1 and "above 10 bits" in r.stdout, r.stdout + r.stderr

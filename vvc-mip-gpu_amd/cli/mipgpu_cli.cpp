@@ -217,13 +217,16 @@ struct Pinned {
 //  * raw: `luma_only` = consecutive W x H little-endian 16-bit frames; otherwise planar
 //    4:2:0 with 16-bit samples (yuv420p10le), whose two chroma planes (W/2 x H/2 each) are
 //    skipped.
-bool parse_row(const char *p, const char *end, int W, uint16_t *out) {
+// Samples above 10 bits break the engine's input contract (include/mipgpu.h): the row's first
+// such column goes to *bad_x (the engine would report the frame too, after its search).
+bool parse_row(const char *p, const char *end, int W, uint16_t *out, int *bad_x) {
   for (int x = 0; x < W; x++) {
     while (p < end && (*p == ' ' || *p == '\r')) p++;
-    int v = 0;
+    long long v = 0;
     bool any = false;
-    while (p < end && *p >= '0' && *p <= '9') v = v * 10 + (*p++ - '0'), any = true;
+    while (p < end && *p >= '0' && *p <= '9') v = std::min(v * 10 + (*p++ - '0'), 1LL << 40), any = true;
     if (!any) return false;
+    if (v > 1023 && *bad_x < 0) *bad_x = x;
     out[x] = (uint16_t)v;
     while (p < end && *p != ',' && *p != '\n') p++;
     if (p < end && *p == ',') p++;
@@ -280,15 +283,26 @@ class FrameSource {
     }
     start_.push_back(pos_);
     std::vector<char> ok(threads_, 1);
+    std::vector<long long> bad(threads_, -1);  // first out-of-range sample per thread (row * W + x)
     std::vector<std::thread> pool;
     for (int t = 0; t < threads_; t++)
       pool.emplace_back([&, t] {
-        for (size_t r = t; r < rows; r += threads_)
-          if (!parse_row(data + start_[r], data + start_[r + 1], W_, out + r * W_)) ok[t] = 0;
+        for (size_t r = t; r < rows; r += threads_) {
+          int bx = -1;
+          if (!parse_row(data + start_[r], data + start_[r + 1], W_, out + r * W_, &bx)) ok[t] = 0;
+          if (bx >= 0 && bad[t] < 0) bad[t] = (long long)r * W_ + bx;
+        }
       });
     for (auto &th : pool) th.join();
+    for (long long b : bad)
+      if (b >= 0 && (range_bad_ < 0 || b + frames_read_ * (long long)fs < range_bad_))
+        range_bad_ = b + frames_read_ * (long long)fs;
+    frames_read_ += n;
+    if (range_bad_ >= 0) return false;
     return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
   }
+  // First sample above 10 bits (frame * W * H + row * W + x), or -1.
+  long long range_error() const { return range_bad_; }
 
  private:
   int W_ = 0, H_ = 0, threads_ = 1;
@@ -298,6 +312,7 @@ class FrameSource {
   void *map_ = nullptr;
   size_t size_ = 0, pos_ = 0;
   std::vector<size_t> start_;
+  long long range_bad_ = -1, frames_read_ = 0;
 };
 
 std::string input_format(const Options &o) {
@@ -711,6 +726,13 @@ int main(int argc, char **argv) {
   fclose(log_fp);
   if (best_fp) fclose(best_fp);
   const bool bin_ok = !bin_fp || fclose(bin_fp) == 0;
+  if (read_failed && src.range_error() >= 0) {
+    const long long b = src.range_error(), fs1 = (long long)W * H;
+    std::cout << "  [!] ERROR: input sample " << b / fs1 << ":" << (b % fs1) / W << ":" << b % W
+              << " (frame:row:column) is above 10 bits (> 1023); samples must be 10-bit values" << std::endl;
+    destroy_all();
+    return 1;
+  }
   if (read_failed) {
     perror("error while opening samples files");
     destroy_all();

@@ -93,7 +93,15 @@ struct SearchArgs {
   uint32_t chunks;        // queue chunks, 1..kQueueChunks (set by launch_search)
   uint64_t *wave_clock;   // profiling (MIPGPU_WAVE_TIMING): [workgroup][kClockSlots] cycles per
                           // task of the workgroup's list; else null
+  // Input contract (samples are 10-bit): a workgroup that stages an original sample above
+  // 1023 stores 1 to status[kStatusOrig], a caller-supplied reference sample above 1023
+  // (check_refs) 1 to status[kStatusRefs].  status is engine-owned page-locked host memory
+  // (read by the host after the search; only ever written when the contract is broken).
+  uint32_t *status;
+  int check_refs;
 };
+constexpr int kStatusOrig = 0, kStatusRefs = 1, kStatusWords = 4;
+constexpr uint32_t kAbove10Bits = 0xfc00fc00u;  // any of bits 10..15 in either half
 constexpr int kClockSlots = 128;
 // Item queue of one launch: the items are cut into kQueueChunks contiguous chunks, one per
 // XCD (workgroups b and b + 8 share an XCD), each with its own counter (mip_search.hip

@@ -1327,17 +1327,30 @@ struct WindowStager {
 
 // (whole workgroup, kWaves * 64 threads: every thread's loads are issued before its first
 // LDS store, so the workgroup waits for HBM once, not once per load)
+// Input contract: a staged sample above 10 bits (any of bits 10..15 of the OR of the
+// loaded chunks) marks the search's status word (SearchArgs::status); the costs of such a
+// frame are not the reference's (the packed 16-bit / f16 arithmetic is sized for 10 bits), so
+// the host reports the search as failed.  Rare path: one plain store per offending thread.
+__device__ __forceinline__ void flag_above_10_bits(uint32_t bits, uint32_t *status, int word) {
+  if (bits & kAbove10Bits) status[word] = 1u;
+}
+
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
-                                           int x0, int y0) {
+                                           int x0, int y0, uint32_t *status) {
   const WindowStager<64 * kWaves> st(frame, width, height, x0, y0, (int)threadIdx.x);
   constexpr int N = WindowStager<64 * kWaves>::N;
   uint2 v[N];
 #pragma unroll
   for (int k = 0; k < N; k++)
     if (st.valid(k)) v[k] = st.load(k);
+  uint32_t bits = 0;
 #pragma unroll
   for (int k = 0; k < N; k++)
-    if (st.valid(k)) st.store(dst, k, v[k]);
+    if (st.valid(k)) {
+      bits |= v[k].x | v[k].y;
+      st.store(dst, k, v[k]);
+    }
+  flag_above_10_bits(bits, status, kStatusOrig);
 }
 
 // Item = (frame, CTU, quadrant, slice) -> quadrant origin in the frame and frame index.
@@ -1359,8 +1372,10 @@ struct ItemPos {
 
 // Stage the reference lattice (ALT): rows 4i-1 (columns -4..63), columns 4i-1 (rows -1..63),
 // by linear index like the window (frame_chunk).
+// check: caller-supplied references (SearchArgs::check_refs) must be 10-bit too, except frame
+// columns W-2, W-1, whose CUs the exact fixup kernel searches (mipgpu.cpp reads_last_columns).
 __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
-                                              int x0, int y0) {
+                                              int x0, int y0, bool check, uint32_t *status) {
   // all loads first, then all LDS stores (as stage_tile)
   constexpr int NT = 64 * kWaves, kChunks = kPitch / 4, NR = 16 * kChunks, NC = 16 * 65;
   constexpr int NRL = (NR + NT - 1) / NT, NCL = (NC + NT - 1) / NT;
@@ -1377,17 +1392,21 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
     const int fy = y0 + yy - 1, fx = x0 + 4 * col - 1, li = fy * width + fx;  // linear, as frame_chunk
     cv[k] = (fy >= 0 && fx >= 0 && li < width * height) ? frame[li] : 0;
   }
+  uint32_t bits = 0;
 #pragma unroll
   for (int k = 0; k < NRL; k++) {
     const int i = min((int)threadIdx.x + NT * k, NR - 1), row = i / kChunks, ch = i - row * kChunks;
     *reinterpret_cast<uint2 *>(dst + row * kLatRowPitch + 4 * ch) = rv[k];
+    if (check && x0 - kColOff + 4 * ch != width - 4) bits |= rv[k].x | rv[k].y;
   }
   uint16_t *cols = dst + 16 * kLatRowPitch;
 #pragma unroll
   for (int k = 0; k < NCL; k++) {
     const int i = min((int)threadIdx.x + NT * k, NC - 1), col = i / 65, yy = i - col * 65;
     cols[col * kLatColPitch + yy] = cv[k];
+    if (check && x0 + 4 * col - 1 != width - 1) bits |= cv[k];
   }
+  if (check) flag_above_10_bits(bits, status, kStatusRefs);
 }
 
 // Next-item prefetch (PF, non-ALT): two quadrant windows in LDS.  The first wave of an item
@@ -1513,8 +1532,8 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     }
     if (ntasks > 0) {  // workgroup-uniform
       if (!PF || !staged) {
-        stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0);
-        if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0);
+        stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0, a.status);
+        if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0, a.check_refs != 0, a.status);
         __syncthreads();
       }
 
@@ -1583,6 +1602,7 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
           // loads in flight MIP_PF_BATCH at a time, then their stores
           const WindowStager<64> st(nframe, a.width, a.height, np.fx0, np.fy0, lane);
           constexpr int NL = WindowStager<64>::N, NB = MIP_PF_BATCH;
+          uint32_t bits = 0;
 #pragma unroll
           for (int k0 = 0; k0 < NL; k0 += NB) {
             uint2 v[NB];
@@ -1591,8 +1611,12 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
               if (k0 + k < NL && st.valid(k0 + k)) v[k] = st.load(k0 + k);
 #pragma unroll
             for (int k = 0; k < NB; k++)
-              if (k0 + k < NL && st.valid(k0 + k)) st.store(dst, k0 + k, v[k]);
+              if (k0 + k < NL && st.valid(k0 + k)) {
+                bits |= v[k].x | v[k].y;
+                st.store(dst, k0 + k, v[k]);
+              }
           }
+          flag_above_10_bits(bits, a.status, kStatusOrig);
         }
         if (lane == 0) {
           nxt[0] = 0;
@@ -1717,7 +1741,7 @@ int search_resident_groups(bool alt) {
 }
 
 hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, hipStream_t s) {
-  if (args.slices < 1 || !args.queue || resident < 1) return hipErrorInvalidValue;
+  if (args.slices < 1 || !args.queue || !args.status || resident < 1) return hipErrorInvalidValue;
   SearchArgs a = args;
   if (a.ctu0 < 0 || a.nrange < 1 || a.ctu0 + a.nrange > a.nctus) return hipErrorInvalidValue;
   const long long nitems = (long long)(4 * a.slices) * a.nrange * nframes;

@@ -433,6 +433,10 @@ struct mip_engine {
     }
   };
   QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this}};
+  // Input contract (10-bit samples): status words the search kernel sets when it stages a
+  // sample above 1023 (SearchArgs::status), in page-locked host memory mapped into the
+  // device; checked and cleared by check_status.
+  uint32_t *h_status = nullptr, *d_status = nullptr;
 };
 
 namespace {
@@ -451,6 +455,22 @@ const mip_engine::Work &pick_work(const mip_engine *e, int nframes, int nrange) 
   return *best;
 }
 }  // namespace
+
+// Samples above 10 bits seen by a search launched before this point (the kernels mark
+// SearchArgs::status): the costs of that search are not the reference's, so the call that
+// notices reports it (sticky until reported, then cleared).  The reference reads the CSV
+// samples into unsigned short and its kernels take short* (main.cpp:364-384, intra.cl:17,
+// 545), with 10-bit constants throughout (constants.cl:22-23, valueDC = 512, clip 1023);
+// this engine's packed 16-bit / f16 arithmetic is exact for 10-bit samples only.
+static int check_status(mip_engine *e) {
+  volatile uint32_t *st = e->h_status;
+  if (!st || !(st[mipgpu::kStatusOrig] | st[mipgpu::kStatusRefs])) return 0;
+  const bool orig = st[mipgpu::kStatusOrig] != 0;
+  st[mipgpu::kStatusOrig] = 0;
+  st[mipgpu::kStatusRefs] = 0;
+  return fail("input contract: %s samples above 10 bits (> 1023) in a frame searched by this engine; its costs are "
+              "not valid (samples must be 10-bit values)", orig ? "frame" : "reference");
+}
 
 // Host-API calls (synchronous) overwrite engine scratch: order them after the device-API
 // searches still reading d_refs; once the call has synchronised both engine streams,
@@ -521,6 +541,7 @@ int mip_engine_destroy(mip_engine *e) {
                   (void *)e->d_ctu_var[0], (void *)e->d_ctu_var[1], (void *)e->d_fixup})
     if (p) (void)hipFree(p);
   if (e->d_queue) (void)hipFree(e->d_queue);
+  if (e->h_status) (void)hipHostFree(e->h_status);
   for (hipEvent_t ev : e->queue_done)
     if (ev) (void)hipEventDestroy(ev);
   if (e->refs_done) (void)hipEventDestroy(e->refs_done);
@@ -608,6 +629,12 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     return cleanup(fail("hipMemset failed"));
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
+  if (hipHostMalloc((void **)&e->h_status, mipgpu::kStatusWords * sizeof(uint32_t),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return cleanup(fail("hipHostMalloc (status words) failed"));
+  memset(e->h_status, 0, mipgpu::kStatusWords * sizeof(uint32_t));
+  if (hipHostGetDevicePointer((void **)&e->d_status, e->h_status, 0) != hipSuccess || !e->d_status)
+    return cleanup(fail("hipHostGetDevicePointer (status words) failed"));
   if (hipEventCreateWithFlags(&e->refs_done, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail("hipEventCreate failed"));
   for (int alt = 0; alt < 2; alt++)
@@ -699,9 +726,13 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
   return 0;
 }
 
+// caller_refs: d_refs holds caller-supplied reference frames (checked against the 10-bit
+// contract like the frames; engine-filtered references are not: the separable filters'
+// defined > 10-bit outputs at the last columns go to the fixup kernel).
 static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
-                              int32_t *d_best_cost, hipStream_t s, int ctu0 = 0, int nrange = -1) {
+                              int32_t *d_best_cost, hipStream_t s, bool caller_refs, int ctu0 = 0,
+                              int nrange = -1) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
   // Decisions only (no cost table): the search writes each CU's decision into d_best /
   // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
@@ -754,6 +785,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.ctu0 = ctu0;
   a.nrange = nrange;
   a.slices = work.slices;
+  a.status = e->d_status;
+  a.check_refs = alt && caller_refs;
   // MIPGPU_WAVE_TIMING=file (profiling): per-task cycles appended to `file` (synchronous;
   // one binary record of uint64 [workgroup][wave][kClockSlots] per launch), and the task
   // lists to `file`.tasks once.
@@ -818,9 +851,17 @@ int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d
                       int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best_mode,
                       int32_t *d_best_cost, void *stream) {
   if (!e) return fail("engine is NULL");
+  if (check_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, d_best_mode, d_best_cost,
-                            (hipStream_t)stream);
+                            (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames);
+}
+
+int mip_check_input(mip_engine *e, void *stream) {
+  if (!e) return fail("engine is NULL");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return check_status(e);
 }
 
 int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
@@ -830,9 +871,11 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
   if (!d_costs) return fail("d_costs is NULL");
   // an empty range (more CTU-row bands than CTU rows, mipgpu.split) is a successful no-op
   if (ctu_begin == ctu_end && ctu_begin >= 0 && ctu_end <= e->nctus) return 0;
+  if (check_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, nullptr, nullptr,
-                            (hipStream_t)stream, ctu_begin, ctu_end - ctu_begin);
+                            (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames, ctu_begin,
+                            ctu_end - ctu_begin);
 }
 
 static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
@@ -861,6 +904,7 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
   if (!e || !frames || nframes < 1 || !ticket) return fail("bad search arguments");
   *ticket = 0;
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
+  if (check_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
   const int rc = search_frames_chunks(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out,
                                       sad_out, satd_out, e->host_calls + 1);
@@ -996,7 +1040,8 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     int32_t *d_sad = sad_out ? e->d_sad + fo * cpf : nullptr, *d_satd = satd_out ? e->d_satd + fo * cpf : nullptr;
     uint8_t *d_best = best_mode_out ? e->d_best + fo * upf : nullptr;
     int32_t *d_best_cost = best_cost_out || decisions_only ? e->d_best_cost + fo * upf : nullptr;
-    if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp) != 0)
+    if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
+                           refs_or_null != nullptr) != 0)
       return -1;
     HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     if (!any_out) continue;
@@ -1020,7 +1065,7 @@ int mip_wait(mip_engine *e, uint64_t ticket) {
   HIP_TRY(hipEventSynchronize(e->call_done[(ticket - 1) % mip_engine::kCallRing]));
   // pageable outputs: copy the call's staged downloads out (and everything queued before)
   HIP_TRY(e->stage.drain(ticket));
-  return 0;
+  return check_status(e);
 }
 
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
@@ -1107,7 +1152,8 @@ double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uin
   if (hipEventCreate(&t0) != hipSuccess || hipEventCreate(&t1) != hipSuccess) return fail("hipEventCreate");
   (void)hipEventRecord(t0, e->stream);
   for (int r = 0; r < reps; r++)
-    if (search_device_impl(e, d_frames, d_refs, nframes, d_costs, nullptr, nullptr, nullptr, nullptr, e->stream) != 0) {
+    if (search_device_impl(e, d_frames, d_refs, nframes, d_costs, nullptr, nullptr, nullptr, nullptr, e->stream,
+                           d_refs != nullptr && d_refs != d_frames) != 0) {
       (void)hipEventDestroy(t0);
       (void)hipEventDestroy(t1);
       return -1;
@@ -1118,6 +1164,7 @@ double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uin
   (void)hipEventElapsedTime(&ms, t0, t1);
   (void)hipEventDestroy(t0);
   (void)hipEventDestroy(t1);
+  if (check_status(e) != 0) return -1;
   return ms / reps;
 }
 

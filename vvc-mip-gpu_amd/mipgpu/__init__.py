@@ -86,6 +86,7 @@ def library():
         "mip_wait": (ip, [vp, ctypes.c_uint64]),
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
         "mip_search_device_range": (ip, [vp, vp, vp, ip, ip, ip, vp, vp, vp, vp]),
+        "mip_check_input": (ip, [vp, vp]),
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
         "mip_topk_device": (ip, [vp, ip, ip, ip, ip, vp, vp, vp]),
         "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
@@ -293,6 +294,13 @@ class MipEngine:
                                                  int(ctu_end), _ptr(costs), _ptr(sad), _ptr(satd),
                                                  ctypes.c_void_p(s.cuda_stream)))
         return costs
+
+    def check_input(self, stream=None):
+        """Input contract of the device-API searches on `stream` (mip_check_input): waits for
+        the stream and raises MipError if a search staged a sample above 1023 (10 bits)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        _check(library().mip_check_input(self._h, ctypes.c_void_p(s.cuda_stream)))
 
     def time_search_device(self, frames, costs, refs=None, reps=10) -> float:
         ms = library().mip_time_search_device(self._h, _ptr(frames), _ptr(refs), frames.shape[0], _ptr(costs),
