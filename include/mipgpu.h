@@ -29,8 +29,9 @@
  * with the 47 CU shapes in reference order.  Samples are addressed like the reference does,
  * by linear index y * width + x, so CUs right of the frame (widths that are not multiples
  * of 128) read the next row's samples and get the reference's costs.  CUs whose cost the
- * reference leaves undefined -- below the frame (stale LDS, intra.cl:96-98) or reading past
- * the frame's end -- are reported as MIP_COST_UNAVAILABLE.
+ * reference leaves undefined -- below the frame (stale LDS, intra.cl:96-98), reading past
+ * the frame's end, or (engine filter) reading a filtered sample computed from past the
+ * frame's end -- are reported as MIP_COST_UNAVAILABLE (mip_unavailable_cus lists them).
  */
 #ifndef MIPGPU_H
 #define MIPGPU_H
@@ -91,6 +92,19 @@ const char *mip_shape_name(int shape);                       /* main_aux_functio
 int mip_shape_info(int shape, int *w, int *h, int *modes, int *ncu, int *cost_offset);
 /* CTU-relative position of CU `cu` of `shape` (ALL_X_POS / ALL_Y_POS, constants.h:1235-1354). */
 int mip_cu_position(int shape, int cu, int *x, int *y);
+
+/* CUs whose costs this engine reports as MIP_COST_UNAVAILABLE for width x height frames,
+ * with references from the engine's own filter `filter` (MIP_FILTER_NONE: original
+ * references): 1 per CU in the order ctu*5380 + shape CU prefix + cu, for nCTUs*5380 CUs.
+ * They are the CUs the reference leaves undefined geometrically (below the frame, stale LDS
+ * intra.cl:96-98; reading past the frame's end) and, with a filter, the CUs that read a
+ * filtered sample the reference's filter computes from memory past the frame's end (its
+ * linear tile addressing, intra.cl:2904-2909 / 3330-3332; e.g. the last frame row of the
+ * separable 3-tap filters when the height is not a multiple of 32).  Filtered samples that
+ * two of the reference's tiles store with different values (widths that are not multiples
+ * of 128, intra.cl:3037) are not undefined here: the engine uses the owning tile's value,
+ * one of the reference's two outcomes.  Host only; returns 0 or <0. */
+int mip_unavailable_cus(int width, int height, int filter, uint8_t *cu_out);
 
 /* Low-pass filter of `nframes` host frames (filterFrame_<type>, main.cpp:700-761).
  * out must hold nframes frames.  Synchronous. */

@@ -607,7 +607,8 @@ static void tile_sep5(const uint16_t *in, int W, int H, int X, int Y, const uint
  * row, over samples another work-group writes: the two stores race.  Where both values
  * agree the sample is well defined; where they differ (or either is poison) the reference's
  * result depends on the work-groups' timing and the sample is marked undefined.  `undef`
- * (may be NULL) receives 1 for undefined samples (poison or race). */
+ * (may be NULL) receives, per sample, bit 0 = poison (reads past the frame's end), bit 1 =
+ * race with a different value (0 = defined). */
 static int filter_run(const uint16_t *in, uint16_t *out, uint8_t *undef, int W, int H, int filter, int kernel_idx) {
   const int five = filter >= MIPO_FILTER_1D_INT_5x5;
   const int sep = filter == MIPO_FILTER_1D_INT || filter == MIPO_FILTER_1D_FLOAT || filter == MIPO_FILTER_1D_INT_5x5 ||
@@ -638,8 +639,9 @@ static int filter_run(const uint16_t *in, uint16_t *out, uint8_t *undef, int W, 
             if (!pass) {
               out[idx] = v;
               und[idx] = op[r * 128 + c];
-            } else if (op[r * 128 + c] || v != out[idx]) {
-              und[idx] = 1;
+            } else {
+              if (op[r * 128 + c]) und[idx] |= 1;
+              if (v != out[idx]) und[idx] |= 2;
             }
           }
       }

@@ -69,9 +69,11 @@ def clip_counts(reset=True):
     return int(out[0]), int(out[1])
 
 
-def filter_frame(frame, filter_name, kernel_idx, with_undefined=False):
+def filter_frame(frame, filter_name, kernel_idx, with_undefined=False, kinds=False):
     """Oracle filter.  with_undefined: also return the bool mask of samples the reference
-    leaves undefined (reads past the frame end, racing stores; mipo_filter_frame_ex)."""
+    leaves undefined (reads past the frame end, racing stores; mipo_filter_frame_ex); kinds:
+    that mask as codes instead (bit 0 = poison: reads past the frame's end, bit 1 = a racing
+    store with a different value)."""
     frame = np.ascontiguousarray(frame, np.uint16)
     out = np.zeros_like(frame)
     und = np.zeros(frame.shape, np.uint8)
@@ -79,7 +81,23 @@ def filter_frame(frame, filter_name, kernel_idx, with_undefined=False):
                                     kernel_idx)
     if rc != 0:
         raise ValueError(f"oracle filter {filter_name}/{kernel_idx} unsupported (rc={rc})")
-    return (out, und.astype(bool)) if with_undefined else out
+    if not with_undefined:
+        return out
+    return out, (und if kinds else und.astype(bool))
+
+
+def engine_unavailable_mask(frame, filter_name, kernel_idx):
+    """Entries the engine reports MIP_COST_UNAVAILABLE when it filters the references itself:
+    the geometrically undefined CUs and the CUs that read a filtered sample the reference's
+    filter computes from memory past the frame's end (poison, bit 0 of the oracle's codes).
+    CUs whose reference samples only race (bit 1) get the owning tile's value, one of the
+    reference's outcomes."""
+    from mipgpu import layout
+    w, h = frame.shape[1], frame.shape[0]
+    if filter_name is None:
+        return ~layout.available_mask(w, h)
+    _, und = filter_frame(frame, filter_name, kernel_idx, with_undefined=True, kinds=True)
+    return ~defined_mask(w, h, (und & 1).astype(bool))
 
 
 def defined_mask(width, height, refs_undefined=None):
@@ -99,3 +117,21 @@ def synth(width, height, seed, kind=0):
     out = np.zeros((height, width), np.uint16)
     lib().mipo_synth_frame(out, width, height, seed, kind)
     return out
+
+
+def engine_search(orig, filter_name=None, kernel_idx=0, ctus=None, want_sad_satd=False, nthreads=0):
+    """What the engine returns when it filters the references itself (filter_name) or uses
+    the originals (None): the oracle's search with the engine's UNAVAILABLE entries
+    (engine_unavailable_mask) filled in."""
+    from mipgpu import layout
+    refs = None if filter_name is None else filter_frame(orig, filter_name, kernel_idx)
+    res = search(orig, refs, ctus=ctus, want_sad_satd=want_sad_satd, nthreads=nthreads)
+    if filter_name is not None:
+        m = engine_unavailable_mask(orig, filter_name, kernel_idx)
+        if ctus is not None:
+            keep = np.zeros_like(m)
+            keep[ctus[0] * layout.COSTS_PER_CTU:ctus[1] * layout.COSTS_PER_CTU] = True
+            m &= keep
+        for t in (res if want_sad_satd else (res,)):
+            t[m] = layout.UNAVAILABLE
+    return res

@@ -164,8 +164,7 @@ def test_cost_log_is_byte_identical(gpu_available, tmp_path, extra, filt, kidx, 
     assert len(took) == (N if filt else 0)
     assert all(float(ms) > 0 and abs(float(ms) * 1e6 - float(ns)) < 1 for ms, ns in took)
     assert re.search(rf"Elapsed time \(ms\) from writing samples to reading distortion \({N}x\), \d+\n", r.stdout)
-    refs = None if filt is None else O.filter_frame(frames[0], filt, kidx)
-    res = O.search(frames[0], refs, want_sad_satd=sad_satd)
+    res = O.engine_search(frames[0], filt, kidx, want_sad_satd=sad_satd)
     cost, sad, satd = res if sad_satd else (res, None, None)
     cost = mask_unavailable(cost, W, H)
     if sad_satd:

@@ -53,8 +53,7 @@ def test_banded_search_equals_whole_frame(gpu_available, filt, k, parts):
         got = banded.cpu().numpy()
     assert np.array_equal(got, whole)
     for f in range(n):
-        refs = O.filter_frame(frames[f], filt, k) if filt else None
-        assert np.array_equal(whole[f], O.search(frames[f], refs))
+        assert np.array_equal(whole[f], O.engine_search(frames[f], filt, k))
 
 
 def _gather_worker(rank, world, port, q):

@@ -189,24 +189,129 @@ bool reads_last_columns(int width, int height, int x, int y, int w, int h) {
   return false;
 }
 
-// CTU -> variant = index of the CTU's set of CUs the search kernel computes (the others get
-// MIP_COST_UNAVAILABLE from the fill lists; the fixup kernel overwrites its CUs after).
-// Two maps share the variants: original references ([0]: every defined CU) and alternative
-// references ([1]: minus the fixup CUs when the width is not a multiple of 128).
-struct CtuVariants {
-  std::vector<uint8_t> of_ctu[2];
-  std::vector<std::vector<bool>> pattern;  // [variant][CU in CTU order]
-  std::vector<mipgpu::FixupCu> fixup;      // ALT: CUs computed by the fixup kernel
+// Filtered reference samples the reference leaves undefined because the filter reads memory
+// past the frame's end ("poison"; the oracle's mipo_filter_frame_ex models the same and
+// tests/test_gpu_parity.py compares the two).  The reference's filters work on 128x32 tiles
+// (intra.cl:2873-2879) and address the frame by linear index; halo cells are gated by
+// index < W*H (2D intra.cl:2913-2966 / 3103-3189 and float twins; separable 3336-3366,
+// 3606-3688), so only interior cells can read past the end:
+//   2-D and separable 5-tap: rows inside the frame are read (2904-2909, 3595-3598), so only
+//     the last row right of the frame (wrapping past the end) -- at widths that are not
+//     multiples of 128;
+//   separable 3-tap: interior rows are read unguarded (3330-3332), so every row below the
+//     frame (last tile band when H % 32 != 0) too.
+// An output depends on the cells of its window (2-D: (2R+1)^2; separable: horizontal taps of
+// the vertical taps' rows, 3377-3478 / 3705-3788).  Tiles store all their 128 columns by
+// linear index (3027-3038, 3489-3505): the last tile column's columns right of the frame land
+// on the next row, so their poison counts there too (where the two stores race with defined
+// values, the engine keeps the owning tile's value: one of the reference's outcomes).
+// Only the last tile band (rows [y0, H)) holds such cells; returned as a mask over it.
+struct Poison {
+  int y0 = 0;                  // first frame row of the mask
+  std::vector<uint8_t> mask;   // [(H - y0) * W]: 1 = undefined (linear index - y0 * W)
+  bool any = false;
+  bool at(long long li, int width) const {
+    const long long o = li - (long long)y0 * width;
+    return o >= 0 && o < (long long)mask.size() && mask[(size_t)o];
+  }
 };
 
-CtuVariants ctu_variants(int width, int height) {
+Poison filter_poison(int width, int height, int filter) {
+  Poison ps;
+  if (filter < 0) return ps;
+  const bool sep = filter == MIP_FILTER_1D_INT || filter == MIP_FILTER_1D_FLOAT || filter == MIP_FILTER_1D_INT_5x5 ||
+                   filter == MIP_FILTER_1D_FLOAT_5x5;
+  const bool five = filter >= MIP_FILTER_1D_INT_5x5;
+  const long long W = width, H = height, WH = W * H;
+  ps.y0 = 32 * ((height - 1) / 32);
+  ps.mask.assign((size_t)(H - ps.y0) * W, 0);
+  const int qy = ps.y0, rows = std::min(32, height - qy);
+  // cell poison of tile rows ty (interior 0..31) at tile column tc (0..127)
+  auto cell = [&](int qx, int ty, int tc) -> bool {
+    if (ty < 0 || ty >= 32 || tc < 0 || tc >= 128) return false;  // halo: gated, never poison
+    const long long y = qy + ty;
+    if (!(sep && !five) && y >= H) return false;  // 2-D / 5-tap separable: rows below not read
+    return y * W + qx + tc >= WH;
+  };
+  const int R = five ? 2 : 1;
+  for (int qx = 0; qx < width; qx += 128) {
+    uint8_t out[32][128] = {};
+    bool tile_any = false;
+    for (int r = 0; r < rows; r++)
+      for (int c = 0; c < 128; c++) {
+        bool p = false;
+        if (!sep) {
+          for (int dy = -R; dy <= R && !p; dy++)
+            for (int dx = -R; dx <= R && !p; dx++) p = cell(qx, r + dy, c + dx);
+        } else {
+          // vertical taps over rows r-R..r+R (5-tap: only rows with a horizontal pass,
+          // i.e. frame rows, intra.cl:3705-3726), horizontal taps c-R..c+R of each
+          for (int dy = -R; dy <= R && !p; dy++) {
+            if (five && (qy + r + dy < 0 || qy + r + dy >= height)) continue;
+            for (int dx = -R; dx <= R && !p; dx++) p = cell(qx, r + dy, c + dx);
+          }
+        }
+        out[r][c] = p;
+        tile_any |= p;
+      }
+    if (!tile_any) continue;
+    for (int r = 0; r < rows; r++)
+      for (int c = 0; c < 128; c++) {
+        const long long li = (long long)(qy + r) * W + qx + c;  // owning or wrapped store
+        if (out[r][c] && li < WH) {
+          ps.mask[(size_t)(li - (long long)qy * W)] = 1;
+          ps.any = true;
+        }
+      }
+  }
+  return ps;
+}
+
+// Does the CU at frame position (x, y) read a poisoned reference sample (its top row or the
+// top-edge padding sample, its left column or the left-edge padding sample, by linear index
+// as the reference's initBoundaries does, intra.cl:96-107, 232-243)?
+bool reads_poison(const Poison &ps, int width, int x, int y, int w, int h) {
+  if (!ps.any) return false;
+  if (y > 0) {
+    for (int i = 0; i < w; i++)
+      if (ps.at((long long)(y - 1) * width + x + i, width)) return true;
+  } else if (x > 0 && ps.at(x - 1, width)) {
+    return true;
+  }
+  if (x > 0) {
+    for (int i = 0; i < h; i++)
+      if (ps.at((long long)(y + i) * width + x - 1, width)) return true;
+  } else if (y > 0 && ps.at((long long)(y - 1) * width, width)) {
+    return true;
+  }
+  return false;
+}
+
+// CTU -> variant = index of the CTU's set of CUs the search kernel computes (the others get
+// MIP_COST_UNAVAILABLE from the fill lists; the fixup kernel overwrites its CUs after).
+// Three maps share the variants (kMapOrig / kMapAltCaller / kMapAltEngine): original
+// references (every defined CU); caller-supplied alternative references (minus the fixup CUs
+// when the width is not a multiple of 128); the engine filter's references (minus the fixup
+// CUs and minus the CUs that read a sample the reference's filter leaves undefined,
+// filter_poison -- those are MIP_COST_UNAVAILABLE).
+constexpr int kMapOrig = 0, kMapAltCaller = 1, kMapAltEngine = 2, kMaps = 3;
+struct CtuVariants {
+  std::vector<uint8_t> of_ctu[kMaps];
+  std::vector<std::vector<bool>> pattern;         // [variant][CU in CTU order]
+  std::vector<mipgpu::FixupCu> fixup[kMaps];      // ALT: CUs computed by the fixup kernel
+};
+
+CtuVariants ctu_variants(int width, int height, int filter) {
   CtuVariants v;
   const int cols = (width + 127) / 128, n = cols * ((height + 127) / 128);
-  for (int alt = 0; alt < 2; alt++)
+  const Poison ps = filter_poison(width, height, filter);
+  for (int map = 0; map < kMaps; map++)
     for (int c = 0; c < n; c++) {
       const int cx = 128 * (c % cols), cy = 128 * (c / cols);
       // only CTUs whose CUs reach the last columns can hold fixup CUs (wraps: W < 256)
-      const bool near_edge = alt && width % 128 && (cx + 256 >= width || width < 256);
+      const bool near_edge = map != kMapOrig && width % 128 && (cx + 256 >= width || width < 256);
+      // only CTUs whose CUs reach the poisoned band (one CTU row up: left columns wrap)
+      const bool near_poison = map == kMapAltEngine && ps.any && cy + 256 > ps.y0;
       std::vector<bool> pat;
       pat.reserve(MIP_CUS_PER_CTU);
       int k = 0;
@@ -215,9 +320,10 @@ CtuVariants ctu_variants(int width, int height) {
         for (int cu = 0; cu < sd.ncu; cu++, k++) {
           const int lx = axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), ly = axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
           bool on = cu_defined(width, height, cx + lx, cy + ly, sd.w, sd.h);
+          if (on && near_poison && reads_poison(ps, width, cx + lx, cy + ly, sd.w, sd.h)) on = false;
           if (on && near_edge && reads_last_columns(width, height, cx + lx, cy + ly, sd.w, sd.h)) {
             on = false;
-            v.fixup.push_back(mipgpu::FixupCu{(uint32_t)c, (uint16_t)k, (uint8_t)s, 0});
+            v.fixup[map].push_back(mipgpu::FixupCu{(uint32_t)c, (uint16_t)k, (uint8_t)s, 0});
           }
           pat.push_back(on);
         }
@@ -225,7 +331,7 @@ CtuVariants ctu_variants(int width, int height) {
       size_t var = 0;
       while (var < v.pattern.size() && v.pattern[var] != pat) var++;
       if (var == v.pattern.size()) v.pattern.push_back(pat);
-      v.of_ctu[alt].push_back((uint8_t)std::min<size_t>(var, 255));
+      v.of_ctu[map].push_back((uint8_t)std::min<size_t>(var, 255));
     }
   return v;
 }
@@ -407,9 +513,10 @@ struct mip_engine {
   };
   std::vector<Work> work;
   uint8_t *d_tables = nullptr;
-  uint8_t *d_ctu_var[2] = {nullptr, nullptr};  // [orig / alt refs][nctus] CTU variant (ctu_variants)
-  mipgpu::FixupCu *d_fixup = nullptr;          // alt refs: CUs of the exact per-CU kernel
-  int nfixup = 0;
+  uint8_t *d_ctu_var[kMaps] = {};           // [map][nctus] CTU variant (ctu_variants: orig /
+                                            // caller refs / engine-filtered refs)
+  mipgpu::FixupCu *d_fixup[kMaps] = {};     // alt refs: CUs of the exact per-CU kernel, per map
+  int nfixup[kMaps] = {};
   int resident[2] = {0, 0};  // persistent search grid (workgroups resident on this device), [alt]
   // Engine-owned reference scratch d_refs, written by the engine filter when a device-API
   // search has no caller references: every such search records refs_done on its stream, and
@@ -520,6 +627,25 @@ int mip_shape_info(int shape, int *w, int *h, int *modes, int *ncu, int *cost_of
   return 0;
 }
 
+int mip_unavailable_cus(int width, int height, int filter, uint8_t *cu_out) {
+  if (!cu_out || width <= 0 || height <= 0 || width % 4 || height % 4) return fail("bad unavailable-CU arguments");
+  if (filter < MIP_FILTER_NONE || filter > MIP_FILTER_2D_FLOAT_5x5) return fail("invalid filter %d", filter);
+  const Poison ps = filter_poison(width, height, filter);
+  const int cols = (width + 127) / 128, n = mip_num_ctus(width, height);
+  size_t k = 0;
+  for (int c = 0; c < n; c++) {
+    const int cx = 128 * (c % cols), cy = 128 * (c / cols);
+    for (int s = 0; s < MIP_NUM_SHAPES; s++) {
+      const mip_shape_desc &sd = kShapes[s];
+      for (int cu = 0; cu < sd.ncu; cu++, k++) {
+        const int x = cx + axis_pos(sd.xb, sd.xs, sd.xd, cu % sd.ncols), y = cy + axis_pos(sd.yb, sd.ys, sd.yd, cu / sd.ncols);
+        cu_out[k] = !cu_defined(width, height, x, y, sd.w, sd.h) || reads_poison(ps, width, x, y, sd.w, sd.h);
+      }
+    }
+  }
+  return 0;
+}
+
 int mip_cu_position(int shape, int cu, int *x, int *y) {
   if (shape < 0 || shape >= MIP_NUM_SHAPES) return fail("bad shape index %d", shape);
   const mip_shape_desc &s = kShapes[shape];
@@ -537,9 +663,12 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream3) (void)hipStreamSynchronize(e->stream3);
   e->stage.abandon();
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
-                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables,
-                  (void *)e->d_ctu_var[0], (void *)e->d_ctu_var[1], (void *)e->d_fixup})
+                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables})
     if (p) (void)hipFree(p);
+  for (int m = 0; m < kMaps; m++) {
+    if (e->d_ctu_var[m]) (void)hipFree(e->d_ctu_var[m]);
+    if (e->d_fixup[m]) (void)hipFree(e->d_fixup[m]);
+  }
   if (e->d_queue) (void)hipFree(e->d_queue);
   if (e->h_status) (void)hipHostFree(e->h_status);
   for (hipEvent_t ev : e->queue_done)
@@ -641,20 +770,20 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0)) < 1)
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
-  const CtuVariants cv = ctu_variants(width, height);
+  const CtuVariants cv = ctu_variants(width, height, o.filter);
   if (cv.pattern.size() > (size_t)mipgpu::kMaxCtuVariants)
     return cleanup(fail("too many CTU variants (%zu)", cv.pattern.size()));
-  for (int alt = 0; alt < 2; alt++) {
-    ALLOC(e->d_ctu_var[alt], cv.of_ctu[alt].size());
-    if (hipMemcpy(e->d_ctu_var[alt], cv.of_ctu[alt].data(), cv.of_ctu[alt].size(), hipMemcpyHostToDevice) != hipSuccess)
+  for (int m = 0; m < kMaps; m++) {
+    ALLOC(e->d_ctu_var[m], cv.of_ctu[m].size());
+    if (hipMemcpy(e->d_ctu_var[m], cv.of_ctu[m].data(), cv.of_ctu[m].size(), hipMemcpyHostToDevice) != hipSuccess)
       return cleanup(fail("uploading CTU variants failed"));
-  }
-  e->nfixup = (int)cv.fixup.size();
-  if (e->nfixup) {
-    ALLOC(e->d_fixup, cv.fixup.size() * sizeof(mipgpu::FixupCu));
-    if (hipMemcpy(e->d_fixup, cv.fixup.data(), cv.fixup.size() * sizeof(mipgpu::FixupCu), hipMemcpyHostToDevice) !=
-        hipSuccess)
-      return cleanup(fail("uploading fixup CUs failed"));
+    e->nfixup[m] = (int)cv.fixup[m].size();
+    if (e->nfixup[m]) {
+      ALLOC(e->d_fixup[m], cv.fixup[m].size() * sizeof(mipgpu::FixupCu));
+      if (hipMemcpy(e->d_fixup[m], cv.fixup[m].data(), cv.fixup[m].size() * sizeof(mipgpu::FixupCu),
+                    hipMemcpyHostToDevice) != hipSuccess)
+        return cleanup(fail("uploading fixup CUs failed"));
+    }
   }
   std::vector<int> slice_set;
   if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
@@ -777,7 +906,10 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.dfill = work.d_dfill;
   a.dfill_begin = work.d_dfill_begin;
   a.tables = reinterpret_cast<const uint4 *>(e->d_tables);
-  a.ctu_var = e->d_ctu_var[alt ? 1 : 0];
+  // engine-filtered references (here or in the host pipeline) leave the CUs that read the
+  // filter's undefined samples unavailable; caller-supplied references are taken as they are
+  const int map = !alt ? kMapOrig : (caller_refs ? kMapAltCaller : kMapAltEngine);
+  a.ctu_var = e->d_ctu_var[map];
   a.width = e->width;
   a.height = e->height;
   a.ctu_cols = e->ctu_cols;
@@ -800,7 +932,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     static std::atomic<bool> dumped{false};
     if (!dumped.exchange(true)) {
       const WorkLists wl = build_work(work.slices, mipgpu::search_waves_per_group(), e->width, e->height,
-                                      ctu_variants(e->width, e->height));
+                                      ctu_variants(e->width, e->height, e->opts.filter));
       if (FILE *f = fopen((std::string(timing) + ".tasks").c_str(), "w")) {
         fprintf(f, "{\"slices\": %d, \"list_begin\": [", work.slices);
         for (size_t i = 0; i < wl.list_begin.size(); i++) fprintf(f, "%s%d", i ? ", " : "", wl.list_begin[i]);
@@ -824,7 +956,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     return fail("search launch failed: %s", hipGetErrorString(le));
   }
   if (e->queue.launched(slot, s) != 0) return fail("hipEventRecord failed");
-  if (alt && e->nfixup) HIP_TRY(mipgpu::launch_fixup(a, e->d_fixup, e->nfixup, nframes, s));
+  if (alt && e->nfixup[map]) HIP_TRY(mipgpu::launch_fixup(a, e->d_fixup[map], e->nfixup[map], nframes, s));
   if (engine_refs) {
     HIP_TRY(hipEventRecord(e->refs_done, s));
     e->refs_pending = true;

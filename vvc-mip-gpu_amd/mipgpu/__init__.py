@@ -87,6 +87,7 @@ def library():
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
         "mip_search_device_range": (ip, [vp, vp, vp, ip, ip, ip, vp, vp, vp, vp]),
         "mip_check_input": (ip, [vp, vp]),
+        "mip_unavailable_cus": (ip, [ip, ip, ip, vp]),
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
         "mip_topk_device": (ip, [vp, ip, ip, ip, ip, vp, vp, vp]),
         "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
@@ -310,6 +311,15 @@ class MipEngine:
         return ms
 
 
+def unavailable_cus(width, height, filter=None) -> np.ndarray:
+    """Bool per CU (reference order): the CUs an engine with this filter reports as
+    MIP_COST_UNAVAILABLE (mip_unavailable_cus; host only)."""
+    n = num_ctus(width, height) * CUS_PER_CTU
+    out = np.zeros(n, np.uint8)
+    _check(library().mip_unavailable_cus(int(width), int(height), filter_index(filter), out.ctypes.data))
+    return out.astype(bool)
+
+
 def topk_device(costs, width, height, k, modes=None, costs_k=None, stream=None):
     """Per-CU decision lists of device cost tables (torch int32 [F, nCTUs*97840]):
     returns (modes uint8, costs int32), each [F, nCTUs*5380, k] (mip_topk_device)."""
@@ -336,5 +346,5 @@ def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
 
 
 __all__ = ["MipEngine", "MipError", "build_id", "source_id", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "topk_device", "library",
-           "pinned_empty",
+           "pinned_empty", "unavailable_cus",
            "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]
