@@ -11,6 +11,7 @@
 struct Log {
   std::vector<std::string> ev;
   int fail_wait = -1, fail_record = -1, fail_clear = -1;  // slot whose next op fails
+  bool fail_sync = false;                                  // the next sync fails
 };
 
 struct MockOps {
@@ -18,6 +19,12 @@ struct MockOps {
   int wait(int slot, int s) const { return op("wait", slot, s, log->fail_wait); }
   int record(int slot, int s) const { return op("record", slot, s, log->fail_record); }
   int clear(int slot, int s) const { return op("clear", slot, s, log->fail_clear); }
+  int sync(int s) const {
+    log->ev.push_back((log->fail_sync ? "sync!@" : "sync@") + std::to_string(s));
+    const bool f = log->fail_sync;
+    log->fail_sync = false;
+    return f ? 1 : 0;
+  }
   int op(const char *what, int slot, int s, int &fail) const {
     if (fail == slot) {
       fail = -1;
@@ -85,6 +92,38 @@ int main() {
     q.launched(q.acquire(0), 0);  // slot 1
     s = q.acquire(5);
     CHECK(s == 0 && has(l, "wait0@5") && has(l, "clear0@5") && !q.dirty(0));
+  }
+  {  // launch failed vs launched but its record failed: only the latter (a kernel in
+     // flight on the pair) waits for its stream on the host before the slot is reused
+    Log l;
+    QueueRing<MockOps, 2> q{MockOps{&l}};
+    int s = q.acquire(4);
+    q.failed(s);
+    CHECK(!has(l, "sync@4") && q.dirty(s));
+    s = q.acquire(6);
+    l.fail_record = s;
+    CHECK(q.launched(s, 6) != 0 && has(l, "sync@6") && q.dirty(s) && !q.retired(s));
+    q.launched(q.acquire(0), 0);  // slot 0 (cleared first)
+    s = q.acquire(7);             // slot 1: dirty after the sync -> cleared, usable
+    CHECK(s == 1 && has(l, "clear1@7"));
+    // the sync fails too: the slot is retired and skipped from then on
+    l.fail_record = s;
+    l.fail_sync = true;
+    CHECK(q.launched(s, 7) != 0 && q.retired(1));
+    for (int i = 0; i < 4; i++) {
+      const int t = q.acquire(8);
+      CHECK(t == 0);
+      q.launched(t, 8);
+    }
+  }
+  {  // every slot retired: acquire fails
+    Log l;
+    QueueRing<MockOps, 1> q{MockOps{&l}};
+    const int s = q.acquire(0);
+    l.fail_record = s;
+    l.fail_sync = true;
+    q.launched(s, 0);
+    CHECK(q.acquire(0) == -1);
   }
   {  // failing wait / clear are reported and keep the slot dirty
     Log l;

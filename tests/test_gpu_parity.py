@@ -600,3 +600,31 @@ def test_prefetching_launch_equals_small_launches(gpu_available):
         torch.cuda.synchronize()
         assert torch.equal(big, small)
         assert torch.equal(bm, tm[..., 0]) and torch.equal(bc, tc[..., 0])
+
+
+def test_tickets_dropped_on_another_thread(gpu_available):
+    """_Ticket.__del__ waits for its call (mip_wait drains the engine's bounce ring): tickets
+    dropped on a second thread while the first thread runs searches on the same engine are
+    serialised by the engine's lock; every result stays the oracle's."""
+    import gc
+    import threading
+    w, h = 264, 136
+    frames = synth_frames(w, h, 4, 0x7E1, 0)
+    want = np.stack([O.search(frames[f]) for f in range(4)])
+    errors = []
+    with MipEngine(w, h, max_batch=4) as eng:
+        def dropper():
+            try:
+                for i in range(20):
+                    t = eng.search_async(frames[i % 4:i % 4 + 1])  # pageable output: ring drained by wait
+                    del t
+                    gc.collect()
+            except Exception as exc:  # noqa: BLE001
+                errors.append(exc)
+        th = threading.Thread(target=dropper)
+        th.start()
+        for i in range(10):
+            out = eng.search(frames)
+            assert np.array_equal(out["cost"], want), i
+        th.join()
+    assert not errors, errors

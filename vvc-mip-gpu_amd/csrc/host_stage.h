@@ -98,7 +98,13 @@ class CopyPool {
 
 class HostStage {
  public:
-  static constexpr int kRing = 8;
+  // Ring pieces: a chunk's downloads must fit the ring with room for the next chunk's
+  // uploads (kMaxChunkPieces), else enqueueing them would wait on the host for the chunk's
+  // own search and the next upload could not be queued behind it (mipgpu.cpp caps pageable
+  // chunks accordingly).
+  static constexpr int kRing = 16;
+  static constexpr int kMaxChunkPieces = kRing - 4;
+  static constexpr size_t kMaxPiece = 64u << 20;
 
   ~HostStage() {
     if (getenv("MIPGPU_STAGE_STATS"))  // diagnostic: where the staging time goes

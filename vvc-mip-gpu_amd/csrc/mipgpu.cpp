@@ -538,6 +538,7 @@ struct mip_engine {
       return hipMemsetAsync(e->d_queue + mipgpu::kQueueWords * slot, 0, mipgpu::kQueueWords * sizeof(uint32_t), s) !=
              hipSuccess;
     }
+    int sync(hipStream_t s) const { return hipStreamSynchronize(s) != hipSuccess; }
   };
   QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this}};
   // Input contract (10-bit samples): status words the search kernel sets when it stages a
@@ -1103,10 +1104,6 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     const size_t cap = (size_t)(cm && atoi(cm) > 0 ? atoi(cm) : 1024) << 20;
     sb = std::max(1, std::min<int>(sb, (int)(cap / down_per_frame)));
   }
-  {  // equal chunks: a short last chunk would leave the search waiting for the next upload
-    const int nch = (nframes + sb - 1) / sb;
-    sb = (nframes + nch - 1) / nch;
-  }
   const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
   const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
   const bool pin_in = mipgpu::HostStage::pinned(frames) && (!refs_or_null || mipgpu::HostStage::pinned(refs_or_null));
@@ -1115,9 +1112,22 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   const bool pin_satd = !satd_out || mipgpu::HostStage::pinned(satd_out);
   const bool pin_bm = !best_mode_out || mipgpu::HostStage::pinned(best_mode_out);
   const bool pin_bc = !best_cost_out || mipgpu::HostStage::pinned(best_cost_out);
+  // pageable outputs: a chunk's downloads fit the bounce ring beside the next chunk's
+  // uploads (host_stage.h kMaxChunkPieces), so enqueueing them never waits for the chunk's
+  // own search
+  const size_t pageable_down = (size_t)((pin_cost ? 0 : 1) + (pin_sad ? 0 : 1) + (pin_satd ? 0 : 1)) * cpf * 4 +
+                               (pin_bm ? 0 : upf) + (pin_bc ? 0 : upf * 4);
+  if (pageable_down) {
+    const size_t ring = (size_t)mipgpu::HostStage::kMaxChunkPieces * mipgpu::HostStage::kMaxPiece;
+    sb = std::max(1, std::min<int>(sb, (int)(ring / pageable_down)));
+  }
+  {  // equal chunks: a short last chunk would leave the search waiting for the next upload
+    const int nch = (nframes + sb - 1) / sb;
+    sb = (nframes + nch - 1) / nch;
+  }
   if (!(pin_in && pin_cost && pin_sad && pin_satd && pin_bm && pin_bc)) {
     const size_t most = std::max({(size_t)sb * fs * 2, (size_t)sb * cpf * 4, (size_t)sb * upf * 4});
-    HIP_TRY(e->stage.reserve(std::min<size_t>(most, 64u << 20)));
+    HIP_TRY(e->stage.reserve(std::min<size_t>(most, mipgpu::HostStage::kMaxPiece)));
   }
   // host <-> device copy on stream s: DMA from / to page-locked memory, else the bounce ring
   auto to_dev = [&](void *d, const void *h, size_t n, bool pinned) {
@@ -1213,9 +1223,19 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
 int mip_trace_times(mip_engine *e, int enable) {
   if (!e) return fail("engine is NULL");
   HIP_TRY(hipSetDevice(e->device));
-  if (enable && !e->tr_ev[0][0])
-    for (auto &evs : e->tr_ev)
-      for (hipEvent_t &ev : evs) HIP_TRY(hipEventCreate(&ev));
+  if (enable && !e->tr_ev[0][0]) {
+    // all events or none: a partial set would turn tracing on with null events
+    hipEvent_t ev[mip_engine::kHostSlots][4] = {};
+    for (auto &row : ev)
+      for (hipEvent_t &x : row)
+        if (hipEventCreate(&x) != hipSuccess) {
+          for (auto &r2 : ev)
+            for (hipEvent_t y : r2)
+              if (y) (void)hipEventDestroy(y);
+          return fail("hipEventCreate failed (tracing stays off)");
+        }
+    memcpy(e->tr_ev, ev, sizeof ev);
+  }
   e->trace = enable != 0;
   return 0;
 }

@@ -14,7 +14,13 @@
 //   int wait(int slot, Stream s)      stream s waits for the slot's last recorded event
 //   int record(int slot, Stream s)    record the slot's event on s
 //   int clear(int slot, Stream s)     zero the slot's counter pair on s (memset)
+//   int sync(Stream s)                wait on the host until everything queued on s is done
 // each returning 0 on success.
+// A launch that was enqueued but whose event could not be recorded is still running with
+// its pair: no event can order the pair's reuse, so launched() waits for the stream on the
+// host (then the pair is cleared before its next use like a failed launch's); if even that
+// fails, the slot is retired for good -- a later launch on another stream could otherwise
+// clear or share the pair under the running kernel.
 #pragma once
 
 template <class Ops, int kSlots>
@@ -26,7 +32,9 @@ class QueueRing {
   // or -1 if an op failed (the slot is then dirty).
   template <class Stream>
   int acquire(Stream s) {
-    const int slot = (int)(seq_++ % kSlots);
+    int slot = (int)(seq_++ % kSlots);
+    for (int i = 0; i < kSlots && retired_[slot]; i++) slot = (int)(seq_++ % kSlots);
+    if (retired_[slot]) return -1;  // every slot retired
     // the last launch recorded on the slot (a failed one may have recorded nothing: then
     // this waits for an earlier one, which is harmless)
     if (used_[slot] && ops_.wait(slot, s) != 0) {
@@ -46,6 +54,8 @@ class QueueRing {
   int launched(int slot, Stream s) {
     pending_ = -1;
     if (ops_.record(slot, s) != 0) {
+      // the kernel was enqueued: wait for it here, since no event orders the pair's reuse
+      if (ops_.sync(s) != 0) retired_[slot] = true;
       dirty_[slot] = true;
       return -1;
     }
@@ -60,6 +70,7 @@ class QueueRing {
   }
 
   bool dirty(int slot) const { return dirty_[slot]; }
+  bool retired(int slot) const { return retired_[slot]; }
   bool used(int slot) const { return used_[slot]; }
 
  private:
@@ -68,4 +79,5 @@ class QueueRing {
   int pending_ = -1;
   bool used_[kSlots] = {};
   bool dirty_[kSlots] = {};
+  bool retired_[kSlots] = {};
 };

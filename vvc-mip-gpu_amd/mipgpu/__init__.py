@@ -143,7 +143,9 @@ def pinned_empty(shape, dtype) -> np.ndarray:
 class _Ticket:
     """An asynchronous host search in flight: its number, its outputs, and its inputs (kept
     alive until the search has completed).  A ticket dropped without wait() waits in its
-    finaliser, so numpy never frees arrays the engine's copies may still be using."""
+    finaliser, so numpy never frees arrays the engine's copies may still be using.  The
+    finaliser may run on any thread (garbage collection): it takes the engine's lock, like
+    every engine call, because mip_wait drains the engine's bounce ring (not thread safe)."""
 
     def __init__(self, value, out, keep, engine=None):
         self.value, self.out, self._keep, self._engine = value, out, keep, engine
@@ -151,18 +153,25 @@ class _Ticket:
 
     def __del__(self):
         eng = getattr(self, "_engine", None)
-        if not getattr(self, "done", True) and eng is not None and getattr(eng, "_h", None):
-            try:
-                library().mip_wait(eng._h, ctypes.c_uint64(self.value))
-            except Exception:
-                pass
+        if getattr(self, "done", True) or eng is None:
+            return
+        try:
+            with eng._lock:
+                if getattr(eng, "_h", None):
+                    library().mip_wait(eng._h, ctypes.c_uint64(self.value))
+        except Exception:
+            pass
 
 
 class MipEngine:
-    """One engine per GPU (mip_engine_create).  Not thread safe."""
+    """One engine per GPU (mip_engine_create).  Calls on one engine are serialised by a
+    per-engine lock (the C engine must be used by one thread at a time); use one engine per
+    thread for concurrency."""
 
     def __init__(self, width: int, height: int, device: int = 0, filter=None, kernel_idx: int = 0,
                  max_batch: int = 1, want_sad_satd: bool = False, slices_per_ctu: int = 0, best_k: int = 1):
+        import threading
+        self._lock = threading.RLock()
         L = library()
         self.width, self.height = int(width), int(height)
         self.nctus = num_ctus(self.width, self.height)
@@ -179,9 +188,13 @@ class MipEngine:
         self.device = device
 
     def close(self):
-        if getattr(self, "_h", None):
-            library().mip_engine_destroy(self._h)  # synchronises the engine streams first
-            self._h = None
+        lock = getattr(self, "_lock", None)
+        if lock is None:
+            return
+        with lock:
+            if getattr(self, "_h", None):
+                library().mip_engine_destroy(self._h)  # synchronises the engine streams first
+                self._h = None
 
     def __del__(self):
         try:
@@ -250,22 +263,25 @@ class MipEngine:
             if a is not None:
                 res[key] = a
         t = ctypes.c_uint64()
-        _check(library().mip_search_frames_async(self._h, _ptr(f), _ptr(r), n, _ptr(res.get("cost")),
-                                                 _ptr(res.get("best_mode")), _ptr(res.get("best_cost")),
-                                                 _ptr(res.get("sad")), _ptr(res.get("satd")), ctypes.byref(t)))
+        with self._lock:
+            _check(library().mip_search_frames_async(self._h, _ptr(f), _ptr(r), n, _ptr(res.get("cost")),
+                                                     _ptr(res.get("best_mode")), _ptr(res.get("best_cost")),
+                                                     _ptr(res.get("sad")), _ptr(res.get("satd")), ctypes.byref(t)))
         return _Ticket(t.value, res, (f, r), self)
 
     def wait(self, ticket):
         """Block until an asynchronous search has completed; returns its output dict."""
-        _check(library().mip_wait(self._h, ctypes.c_uint64(ticket.value)))
-        ticket.done = True
+        with self._lock:
+            ticket.done = True  # also on error: the call is over either way
+            _check(library().mip_wait(self._h, ctypes.c_uint64(ticket.value)))
         return ticket.out
 
     def filter_frames(self, frames, filter, kernel_idx=0):
         f = self._frames(frames)
         out = np.empty_like(f)
-        _check(library().mip_filter_frames(self._h, _ptr(f), f.shape[0], filter_index(filter), int(kernel_idx),
-                                           _ptr(out)))
+        with self._lock:
+            _check(library().mip_filter_frames(self._h, _ptr(f), f.shape[0], filter_index(filter), int(kernel_idx),
+                                               _ptr(out)))
         return out
 
     # -------------------------------------------------------------- device API
@@ -281,9 +297,10 @@ class MipEngine:
         elif costs is None:
             costs = torch.empty((n, self.costs_per_frame), dtype=torch.int32, device=frames.device)
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
-        _check(library().mip_search_device(self._h, _ptr(frames), _ptr(refs), n, _ptr(costs), _ptr(sad),
-                                           _ptr(satd), _ptr(best_mode), _ptr(best_cost),
-                                           ctypes.c_void_p(s.cuda_stream)))
+        with self._lock:
+            _check(library().mip_search_device(self._h, _ptr(frames), _ptr(refs), n, _ptr(costs), _ptr(sad),
+                                               _ptr(satd), _ptr(best_mode), _ptr(best_cost),
+                                               ctypes.c_void_p(s.cuda_stream)))
         return costs
 
     def search_device_range(self, frames, ctu_begin, ctu_end, costs, refs=None, sad=None, satd=None, stream=None):
@@ -291,9 +308,10 @@ class MipEngine:
         (mip_search_device_range): their blocks of the full-size `costs` are written."""
         import torch
         s = stream if stream is not None else torch.cuda.current_stream(frames.device)
-        _check(library().mip_search_device_range(self._h, _ptr(frames), _ptr(refs), frames.shape[0], int(ctu_begin),
-                                                 int(ctu_end), _ptr(costs), _ptr(sad), _ptr(satd),
-                                                 ctypes.c_void_p(s.cuda_stream)))
+        with self._lock:
+            _check(library().mip_search_device_range(self._h, _ptr(frames), _ptr(refs), frames.shape[0],
+                                                     int(ctu_begin), int(ctu_end), _ptr(costs), _ptr(sad), _ptr(satd),
+                                                     ctypes.c_void_p(s.cuda_stream)))
         return costs
 
     def check_input(self, stream=None):
@@ -301,11 +319,13 @@ class MipEngine:
         the stream and raises MipError if a search staged a sample above 1023 (10 bits)."""
         import torch
         s = stream if stream is not None else torch.cuda.current_stream()
-        _check(library().mip_check_input(self._h, ctypes.c_void_p(s.cuda_stream)))
+        with self._lock:
+            _check(library().mip_check_input(self._h, ctypes.c_void_p(s.cuda_stream)))
 
     def time_search_device(self, frames, costs, refs=None, reps=10) -> float:
-        ms = library().mip_time_search_device(self._h, _ptr(frames), _ptr(refs), frames.shape[0], _ptr(costs),
-                                              int(reps))
+        with self._lock:
+            ms = library().mip_time_search_device(self._h, _ptr(frames), _ptr(refs), frames.shape[0], _ptr(costs),
+                                                  int(reps))
         if ms < 0:
             raise MipError(library().mip_last_error().decode())
         return ms
