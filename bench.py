@@ -264,6 +264,7 @@ def reference_gpu(width, height, frames, seed):
         unit = "frames/s (device time, CL profiling events)" if fb == 0 else \
             "frames/s (host wall time around each kernel: %d CL profiling events unusable)" % fb
         return {"value": round(1000.0 / d["device_ms_per_frame"], 3), "unit": unit, "event_fallbacks": fb,
+                "event_fallback_reason": d.get("event_fallback_reason") or None,
                 "wall_value": round(1000.0 / d["wall_ms_per_frame"], 2),
                 "kernel_ms_per_frame": d["kernel_ms"], "device": d["device"],
                 "note": "reference intra.cl kernels (initBoundaries, MIP_ReducedPred, 3x upsampleDistortion) "

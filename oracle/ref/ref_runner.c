@@ -91,11 +91,15 @@ static cl_program load_program(cl_context ctx, cl_device_id dev, const char *dir
 /* Device time of a finished command from its profiling timestamps; falls back to the
  * host wall time around enqueue+clFinish (passed in) when the timestamps are unusable. */
 static int g_event_fallbacks = 0;
+static char g_fallback_reason[256] = "";
 static double ev_ms(cl_event e, double wall_ms) {
   cl_ulong a = 0, b = 0;
   cl_int e1 = clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_START, sizeof a, &a, NULL);
   cl_int e2 = clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_END, sizeof b, &b, NULL);
   if (e1 != CL_SUCCESS || e2 != CL_SUCCESS || b < a || (double)(b - a) * 1e-6 > 1e3 * wall_ms + 1e3) {
+    if (!g_event_fallbacks) /* the first one, for the report */
+      snprintf(g_fallback_reason, sizeof g_fallback_reason, "start err %d, end err %d, start %llu, end %llu, wall %.4f ms",
+               (int)e1, (int)e2, (unsigned long long)a, (unsigned long long)b, wall_ms);
     g_event_fallbacks++;
     return wall_ms;
   }
@@ -318,9 +322,10 @@ int main(int argc, char **argv) {
   printf("{\"device\": \"%s\", \"width\": %d, \"height\": %d, \"frames\": %d, \"filter\": \"%s\", "
          "\"kernel_ms\": {\"filter\": %.4f, \"initBoundaries\": %.4f, \"MIP_ReducedPred\": %.4f, "
          "\"upsampleDistortion_s2\": %.4f, \"upsampleDistortion_s1\": %.4f, \"upsampleDistortion_s0\": %.4f}, "
-         "\"device_ms_per_frame\": %.4f, \"wall_ms_per_frame\": %.4f, \"event_fallbacks\": %d}\n",
+         "\"device_ms_per_frame\": %.4f, \"wall_ms_per_frame\": %.4f, \"event_fallbacks\": %d, "
+         "\"event_fallback_reason\": \"%s\"}\n",
          dname, W, H, frames, filter ? filter : "", t_filt / frames, t_init / frames, t_red / frames,
          t_up[0] / frames, t_up[1] / frames, t_up[2] / frames, dev_ms / frames, wall * 1e3 / frames,
-         g_event_fallbacks);
+         g_event_fallbacks, g_fallback_reason);
   return 0;
 }
