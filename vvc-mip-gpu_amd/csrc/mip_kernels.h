@@ -90,6 +90,12 @@ struct SearchArgs {
                           // again): [c] next item of chunk c (c < kQueueChunks), then
                           // [kQueueChunks] workgroups done
   uint32_t nitems;        // frames * nrange * 4 * slices (set by launch_search)
+  // Small launches (one queue chunk): item order longest first (LPT).  order[i] = the i-th
+  // (CTU, quadrant, slice) item of a frame, index ctu * 4 * slices + quadrant * slices +
+  // slice, by decreasing estimated cost; queue index q -> item order[q / nframes] of frame
+  // q % nframes.  Null: raster order (frame-major).  Whole-frame launches only.
+  const uint32_t *order;
+  uint32_t nframes;
   uint32_t chunks;        // queue chunks, 1..kQueueChunks (set by launch_search)
   uint64_t *wave_clock;   // profiling (MIPGPU_WAVE_TIMING): [workgroup][kClockSlots] cycles per
                           // task of the workgroup's list; else null

@@ -1358,9 +1358,15 @@ struct ItemPos {
   int frame, ctu, slice, quad, ctu_x, ctu_y, fx0, fy0;
   __device__ __forceinline__ ItemPos(const SearchArgs &a, uint32_t item) {
     const int per_ctu = 4 * a.slices;
-    const int gx = item % per_ctu;
-    ctu = a.ctu0 + (item / per_ctu) % a.nrange;
-    frame = item / (per_ctu * a.nrange);
+    uint32_t base = item;  // item index inside its frame
+    if (a.order) {         // small launches: longest items first, all frames' in turn
+      base = a.order[item / a.nframes];
+      frame = item % a.nframes;
+    } else {
+      frame = item / (per_ctu * a.nrange);
+    }
+    const int gx = base % per_ctu;
+    ctu = a.ctu0 + (base / per_ctu) % a.nrange;
     slice = gx % a.slices;
     quad = gx / a.slices;
     ctu_x = 128 * (ctu % a.ctu_cols);
@@ -1754,6 +1760,8 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   a.chunks = qc && atoi(qc) >= 1 && atoi(qc) <= kQueueChunks
                  ? (uint32_t)atoi(qc)
                  : (a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)resident ? (uint32_t)kQueueChunks : 1u);
+  a.nframes = (uint32_t)nframes;
+  if (a.chunks > 1 || a.ctu0 != 0 || a.nrange != a.nctus) a.order = nullptr;  // large or range launches
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;

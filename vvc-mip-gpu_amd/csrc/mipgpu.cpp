@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
@@ -117,6 +118,8 @@ struct WorkLists {
   std::vector<mipgpu::WaveTask> tasks;
   std::vector<mipgpu::Job> jobs;
   std::vector<int> list_begin;   // [variant][quadrant][slice] + 1
+  std::vector<double> list_cost; // [variant][quadrant][slice]: estimated time of the list on one
+                                 // workgroup (VALU instructions per lane, waves share its tasks)
   std::vector<uint32_t> fill;    // unavailable cost entries, uint4 index inside the CTU block
   std::vector<int> fill_begin;   // [variant][quadrant] + 1
   // decisions only: undefined CUs (CU index inside the CTU) per [variant][quadrant], and the
@@ -447,6 +450,7 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
     for (int b = 0; b < bins; b++) {
       wl.list_begin.push_back((int)wl.tasks.size());
       wl.tasks.insert(wl.tasks.end(), lists[b].begin(), lists[b].end());
+      wl.list_cost.push_back(load[b] / waves);
     }
   }
   wl.list_begin.push_back((int)wl.tasks.size());
@@ -510,8 +514,14 @@ struct mip_engine {
     uint16_t *d_dfill = nullptr, *d_split = nullptr;  // decisions only (WorkLists)
     int *d_dfill_begin = nullptr, *d_split_begin = nullptr;
     int max_split = 0;
+    // Small launches: the frame's items longest first (SearchArgs::order), their estimated
+    // costs in that order (pick_work's makespan model).
+    uint32_t *d_order = nullptr;
+    std::vector<double> order_cost;
   };
   std::vector<Work> work;
+  // pick_work's choice per frame count for small launches (slice count index into `work`)
+  std::vector<int> small_choice;
   uint8_t *d_tables = nullptr;
   uint8_t *d_ctu_var[kMaps] = {};           // [map][nctus] CTU variant (ctu_variants: orig /
                                             // caller refs / engine-filtered refs)
@@ -551,16 +561,56 @@ namespace {
 // CU count limit of one launch (int32 indices in the decision-list kernel).
 constexpr long long kMaxCus = (1LL << 31) - 256;
 
-// Slice count for a launch of `nframes`: items (quadrant x slice) for the persistent grid of
-// 512 workgroups.  Measured on MI355X at 1080p: 1 frame -> 2 slices 5076 frames/s (1: 4842,
-// 4: 4770), >= 2 frames -> 1 slice (2 frames: 5830 vs 5087 with 2 slices).
-const mip_engine::Work &pick_work(const mip_engine *e, int nframes, int nrange) {
-  const long long wg1 = 4LL * nrange * nframes;  // workgroups at one slice
-  const int want = wg1 < 1000 ? 2 : 1;
-  const mip_engine::Work *best = &e->work[0];
-  for (const mip_engine::Work &w : e->work)
-    if (std::abs(w.slices - want) < std::abs(best->slices - want)) best = &w;
-  return *best;
+// Items per workgroup from which a launch cuts its queue into XCD chunks and prefetches
+// (mip_search.hip MIP_PREFETCH_MIN_ITEMS); below it, items are taken longest first.
+constexpr int kSmallLaunchItemsPerGroup = 32;
+// Per-item cost beyond its tasks (window staging, barriers, fills), in the task cost
+// model's units (pair_cost: VALU instructions per lane).
+constexpr double kItemOverhead = 600.0;
+
+bool lpt_order_enabled() {
+  const char *e = getenv("MIPGPU_ORDER");  // A/B knob: 0 = raster item order in small launches
+  return !(e && *e == '0');
+}
+
+// Makespan of `nframes` frames' items taken longest first (SearchArgs::order) by `groups`
+// persistent workgroups: greedy list scheduling of the queue order.
+double lpt_makespan(const std::vector<double> &order_cost, int nframes, int groups) {
+  std::vector<double> fin(groups, 0.0);  // min-heap of finish times
+  for (double c : order_cost)
+    for (int f = 0; f < nframes; f++) {
+      std::pop_heap(fin.begin(), fin.end(), std::greater<double>());
+      fin.back() += c;
+      std::push_heap(fin.begin(), fin.end(), std::greater<double>());
+    }
+  return *std::max_element(fin.begin(), fin.end());
+}
+
+// Slice count for a launch of `nframes`: items (quadrant x slice) for the persistent grid.
+// Large launches (>= kSmallLaunchItemsPerGroup items per workgroup at one slice): one slice.
+// Small ones take their items longest first; the slice count is the one whose predicted
+// makespan (lpt_makespan, per frame count, cached) is the shortest.  (Before the LPT order:
+// 1 frame -> 2 slices 5076 frames/s at 1080p (1: 4842, 4: 4770).)
+const mip_engine::Work &pick_work(mip_engine *e, int nframes, int nrange, int groups) {
+  const long long items1 = 4LL * nrange * nframes;  // items at one slice
+  if (e->work.size() == 1) return e->work[0];
+  if (nrange != e->nctus || items1 >= (long long)kSmallLaunchItemsPerGroup * groups || !lpt_order_enabled()) {
+    const int want = items1 < 1000 && nrange != e->nctus ? 2 : 1;
+    const mip_engine::Work *best = &e->work[0];
+    for (const mip_engine::Work &w : e->work)
+      if (std::abs(w.slices - want) < std::abs(best->slices - want)) best = &w;
+    return *best;
+  }
+  if ((int)e->small_choice.size() <= nframes) e->small_choice.resize(nframes + 1, -1);
+  int &ch = e->small_choice[nframes];
+  if (ch < 0) {
+    double best = 0;
+    for (size_t i = 0; i < e->work.size(); i++) {
+      const double m = lpt_makespan(e->work[i].order_cost, nframes, groups);
+      if (ch < 0 || m < best) ch = (int)i, best = m;
+    }
+  }
+  return e->work[ch];
 }
 }  // namespace
 
@@ -686,7 +736,8 @@ int mip_engine_destroy(mip_engine *e) {
       if (ev) (void)hipEventDestroy(ev);
   for (const mip_engine::Work &w : e->work)
     for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin,
-                    (void *)w.d_dfill, (void *)w.d_dfill_begin, (void *)w.d_split, (void *)w.d_split_begin})
+                    (void *)w.d_dfill, (void *)w.d_dfill_begin, (void *)w.d_split, (void *)w.d_split_begin,
+                    (void *)w.d_order})
       if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -810,6 +861,24 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
         hipMemcpy(ew.d_lists, wl.list_begin.data(), wl.list_begin.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
       return cleanup(fail("uploading work lists failed"));
     ew.max_split = wl.max_split;
+    {  // small launches: the frame's items longest first (original-reference lists' costs)
+      const int per_ctu = 4 * sl;
+      std::vector<double> cost((size_t)e->nctus * per_ctu);
+      for (int c = 0; c < e->nctus; c++)
+        for (int g = 0; g < per_ctu; g++) {
+          const int q = g / sl, slc = g % sl, l = (cv.of_ctu[kMapOrig][c] * 4 + q) * sl + slc;
+          const bool empty = wl.list_begin[l + 1] == wl.list_begin[l];
+          cost[(size_t)c * per_ctu + g] = wl.list_cost[l] + (empty ? kItemOverhead / 8 : kItemOverhead);
+        }
+      std::vector<uint32_t> order(cost.size());
+      for (size_t i = 0; i < order.size(); i++) order[i] = (uint32_t)i;
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+      ew.order_cost.resize(order.size());
+      for (size_t i = 0; i < order.size(); i++) ew.order_cost[i] = cost[order[i]];
+      ALLOC(ew.d_order, order.size() * sizeof(uint32_t));
+      if (hipMemcpy(ew.d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
+        return cleanup(fail("uploading the item order failed"));
+    }
     if (getenv("MIPGPU_WORK_STATS"))  // diagnostic: list sizes per slice count
       fprintf(stderr, "mipgpu work %dx%d slices %d: %zu tasks, %zu jobs, %zu fill, %zu undefined CUs, %zu split CUs (max %d per CTU)\n",
               width, height, sl, wl.tasks.size(), wl.jobs.size(), wl.fill.size(), wl.dfill.size(), wl.split.size(),
@@ -898,7 +967,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.best_cost = decisions_only ? d_best_cost : nullptr;
   a.sad = d_sad;
   a.satd = d_satd;
-  const mip_engine::Work &work = pick_work(e, nframes, nrange);
+  const mip_engine::Work &work = pick_work(e, nframes, nrange, e->resident[alt ? 1 : 0]);
   a.tasks = work.d_tasks;
   a.jobs = work.d_jobs;
   a.list_begin = work.d_lists;
@@ -920,6 +989,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.slices = work.slices;
   a.status = e->d_status;
   a.check_refs = alt && caller_refs;
+  a.order = lpt_order_enabled() ? work.d_order : nullptr;  // launch_search drops it for large / range launches
   // MIPGPU_WAVE_TIMING=file (profiling): per-task cycles appended to `file` (synchronous;
   // one binary record of uint64 [workgroup][wave][kClockSlots] per launch), and the task
   // lists to `file`.tasks once.
