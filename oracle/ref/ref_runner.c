@@ -93,13 +93,18 @@ static cl_program load_program(cl_context ctx, cl_device_id dev, const char *dir
 static int g_event_fallbacks = 0;
 static char g_fallback_reason[256] = "";
 static double ev_ms(cl_event e, double wall_ms) {
-  cl_ulong a = 0, b = 0;
+  cl_ulong a = 0, b = 0, qd = 0, sb = 0, cp = 0;
   cl_int e1 = clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_START, sizeof a, &a, NULL);
   cl_int e2 = clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_END, sizeof b, &b, NULL);
   if (e1 != CL_SUCCESS || e2 != CL_SUCCESS || b < a || (double)(b - a) * 1e-6 > 1e3 * wall_ms + 1e3) {
-    if (!g_event_fallbacks) /* the first one, for the report */
-      snprintf(g_fallback_reason, sizeof g_fallback_reason, "start err %d, end err %d, start %llu, end %llu, wall %.4f ms",
-               (int)e1, (int)e2, (unsigned long long)a, (unsigned long long)b, wall_ms);
+    (void)clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_QUEUED, sizeof qd, &qd, NULL);
+    (void)clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_SUBMIT, sizeof sb, &sb, NULL);
+    (void)clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_COMPLETE, sizeof cp, &cp, NULL);
+    if (!g_event_fallbacks) /* the first one, for the report (relative to QUEUED, ns) */
+      snprintf(g_fallback_reason, sizeof g_fallback_reason,
+               "start err %d, end err %d; ns after queued: submit %lld start %lld end %lld complete %lld; wall %.4f ms",
+               (int)e1, (int)e2, (long long)(sb - qd), (long long)(a - qd), (long long)(b - qd), (long long)(cp - qd),
+               wall_ms);
     g_event_fallbacks++;
     return wall_ms;
   }
