@@ -99,7 +99,7 @@ static double ev_ms(cl_event e, double wall_ms) {
   if (e1 != CL_SUCCESS || e2 != CL_SUCCESS || b < a || (double)(b - a) * 1e-6 > 1e3 * wall_ms + 1e3) {
     (void)clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_QUEUED, sizeof qd, &qd, NULL);
     (void)clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_SUBMIT, sizeof sb, &sb, NULL);
-    (void)clGetEventProfilingInfo(e, CL_PROFILING_COMMAND_COMPLETE, sizeof cp, &cp, NULL);
+    (void)clGetEventProfilingInfo(e, 0x1284 /* CL_PROFILING_COMMAND_COMPLETE, OpenCL 2.0 */, sizeof cp, &cp, NULL);
     if (!g_event_fallbacks) /* the first one, for the report (relative to QUEUED, ns) */
       snprintf(g_fallback_reason, sizeof g_fallback_reason,
                "start err %d, end err %d; ns after queued: submit %lld start %lld end %lld complete %lld; wall %.4f ms",
