@@ -1548,6 +1548,13 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
       // Waves take the item's tasks (longest first) from an LDS counter, so early
       // finishers pick up the slack of waves the SIMD arbiter serves later.
       uint64_t *clk = a.wave_clock ? a.wave_clock + (size_t)item * kClockSlots : nullptr;
+      // profiling: item start / end (s_memrealtime, 100 MHz) and the workgroup's place
+      // (HW_ID: CU / SIMD / SE; XCC_ID) in the last three slots
+      if (clk && threadIdx.x == 0) {
+        clk[kClockSlots - 3] = __builtin_amdgcn_s_memrealtime();
+        clk[kClockSlots - 1] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                               (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
+      }
       for (;;) {
         uint32_t tn = 0;
         if (lane == 0) tn = atomicAdd(next_task, 1u);
@@ -1583,8 +1590,10 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
 #undef MIP_CASE_TR
           default: break;
         }
-        if (clk && lane == 0 && t < kClockSlots) clk[t] = __builtin_readcyclecounter() - c0;
+        if (clk && lane == 0 && t < kClockSlots - 3) clk[t] = __builtin_readcyclecounter() - c0;
       }
+      if (clk && lane == 0) atomicMax(reinterpret_cast<unsigned long long *>(clk + kClockSlots - 2),
+                                      (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
     // ---- next item: its index (and, PF, its window) go to the other parity's slots, which
     // no wave reads during this item
