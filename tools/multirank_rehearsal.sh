@@ -36,4 +36,5 @@ done
 cmp /tmp/mr_out_0.csv /tmp/mr_out_0_0.csv && echo "CLI logs identical (one engine vs two engines on device 0)" | tee "$OUT/cli_cmp.txt"
 sha256sum /tmp/mr_out_0.csv /tmp/mr_out_0_0.csv | tee -a "$OUT/cli_cmp.txt"
 tail -3 "$OUT/cli_dev_0_0.txt"
+rm -f /tmp/mr_out_0.csv /tmp/mr_out_0_0.csv /tmp/mr_in.csv
 echo "== done $(date +%T)"
