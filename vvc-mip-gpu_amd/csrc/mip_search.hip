@@ -700,42 +700,24 @@ struct OrigRows {
     if constexpr (CACHED) return r[i];
     else return *reinterpret_cast<const uint2 *>(row0 + i * kPitch);
   }
-  // Block interface shared with OrigRowsT: row R of the 4x4 block starting at row i0.
-  __device__ __forceinline__ void load_block(int) {}
-  template <int R>
-  __device__ __forceinline__ uint2 at(int i0) const { return (*this)(i0 + R); }
 };
 
 // Original samples of a TR lane's strip: view row i = tile column, re-read per mode pair.
-// A 4x4 view block (view rows i0..i0+3 = tile columns y+i0..y+i0+3, view columns = tile rows
-// x..x+3) is four 8-byte reads of tile rows (load_block); view row R of it is half R & 1 of
-// dword R >> 1 of each (at<R>).  Reading the tile column by column (four 16-bit reads per
-// view row, 68 samples apart) had cost 4x the LDS instructions and 4-8-way bank conflicts
-// (tile rows of one column share banks 2 apart): the transposed classes' LDS waits.
 template <int H>
 struct OrigRowsT {
   static constexpr bool TR = true;
   using Block = BlockAccTr;
   const uint16_t *tile;
   int x, y;  // view coordinates of the strip's first sample
-  uint2 blk[4];  // the current block: blk[k] = tile row x + k, tile columns y + i0 .. + 3
   __device__ __forceinline__ void load(const uint16_t *t, int xx, int yy) {
     tile = t;
     x = xx;
     y = yy;
   }
-  __device__ __forceinline__ void load_block(int i0) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) blk[k] = *reinterpret_cast<const uint2 *>(tile + tidx(y + i0, x + k));
-  }
-  template <int R>
-  __device__ __forceinline__ OrigT at(int) const {
+  __device__ __forceinline__ OrigT operator()(int i) const {
     OrigT o;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t d = (R >> 1) ? blk[k].y : blk[k].x;
-      o.v[k] = (R & 1) ? d >> 16 : d & 0xffff;
-    }
+    for (int k = 0; k < 4; k++) o.v[k] = tile[tidx(y + i, x + k)];
     return o;
   }
 };
@@ -744,18 +726,17 @@ struct OrigRowsT {
 // UV == 1 and 4x4): prediction rows (upsampling, intra.cl:815-912) streamed through the
 // block transform.  `prev` is the anchor row above window k0 (vertical pass state).
 template <int W, int H, int V, class ORIG, class RED, class ACC>
-__device__ __forceinline__ void walk_strip(ORIG &orig, const RED &red, int x0, int k0, int k1, s2 (&prev)[4],
+__device__ __forceinline__ void walk_strip(const ORIG &orig, const RED &red, int x0, int k0, int k1, s2 (&prev)[4],
                                            ACC &acc) {
   using G = Geo<W, H, V>;
   if constexpr (G::SID == 0) {
     // 4x4 CU: the reduced prediction is the prediction (intra.cl:934-936, 995).
     typename ORIG::Block b;
-    orig.load_block(0);
     static_for<4>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
       s2 prow[4];
       red.row4(i, 0, prow);
-      block_row<i>(b, prow, orig.template at<i>(0));
+      block_row<i>(b, prow, orig(i));
     });
     u2 sad, satd;
     block_finish(b, sad, satd);
@@ -767,12 +748,11 @@ __device__ __forceinline__ void walk_strip(ORIG &orig, const RED &red, int x0, i
     for (int bi = 0; bi < G::KV / 4; bi++) {
       const int by = k0 / 4 + bi;
       typename ORIG::Block b;
-      orig.load_block(4 * by);
       static_for<4>([&](auto i_c) {
         constexpr int i = decltype(i_c)::value;
         s2 prow[4];
         anchor_row<W, H>(red, 4 * by + i, x0, prow);
-        block_row<i>(b, prow, orig.template at<i>(4 * by));
+        block_row<i>(b, prow, orig(4 * by + i));
       });
       u2 sad, satd;
       block_finish(b, sad, satd);
@@ -788,7 +768,6 @@ __device__ __forceinline__ void walk_strip(ORIG &orig, const RED &red, int x0, i
     for (int bi = 0; bi < NBLK; bi++) {
       const int by = k0 / 2 + bi;
       typename ORIG::Block b;
-      orig.load_block(4 * by);
       static_for<2>([&](auto hh_c) {
         constexpr int hh = decltype(hh_c)::value;
         const int k = 2 * by + hh;
@@ -796,8 +775,8 @@ __device__ __forceinline__ void walk_strip(ORIG &orig, const RED &red, int x0, i
         anchor_row<W, H>(red, k, x0, next);
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) mid[cc] = avg_round(prev[cc], next[cc]);
-        block_row<2 * hh>(b, mid, orig.template at<2 * hh>(4 * by));
-        block_row<2 * hh + 1>(b, next, orig.template at<2 * hh + 1>(4 * by));
+        block_row<2 * hh>(b, mid, orig(2 * k));
+        block_row<2 * hh + 1>(b, next, orig(2 * k + 1));
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
       });
@@ -827,7 +806,6 @@ __device__ __forceinline__ void walk_strip(ORIG &orig, const RED &red, int x0, i
       static_for<NB>([&](auto bi_c) {
         constexpr int bi = decltype(bi_c)::value;
         typename ORIG::Block b;
-        orig.load_block(k * G::UV + 4 * bi);
         static_for<4>([&](auto i_c) {
           constexpr int i = decltype(i_c)::value, o = 4 * bi + i + 1;
           s2 prow[4];
@@ -840,7 +818,7 @@ __device__ __forceinline__ void walk_strip(ORIG &orig, const RED &red, int x0, i
               prow[cc] = as_s2(as_u2(num[cc]) >> (u2){G::LV, G::LV});
             }
           }
-          block_row<i>(b, prow, orig.template at<i>(k * G::UV + 4 * bi));
+          block_row<i>(b, prow, orig(k * G::UV + 4 * bi + i));
         });
         u2 sad, satd;
         block_finish(b, sad, satd);
@@ -862,7 +840,7 @@ constexpr bool kPaired = Geo<W, H, V>::SID != 0 && W * H >= MIP_PAIR_MIN_AREA &&
                          ((Geo<W, H, V>::CHUNKED ? 4 * Geo<W, H, V>::UV : Geo<W, H, V>::KV * Geo<W, H, V>::UV) / 4) % 2 == 0;
 
 template <int W, int H, int V, class ORIG, class RED>
-__device__ __forceinline__ void walk_pairs(ORIG &orig, const RED &red, int x0, int k0, s2 (&prev)[4],
+__device__ __forceinline__ void walk_pairs(const ORIG &orig, const RED &red, int x0, int k0, s2 (&prev)[4],
                                            PairAcc &acc) {
   using G = Geo<W, H, V>;
   constexpr int ROWS = G::CHUNKED ? 4 * G::UV : G::KV * G::UV;  // CU rows of this call
@@ -878,15 +856,14 @@ __device__ __forceinline__ void walk_pairs(ORIG &orig, const RED &red, int x0, i
     // emit(i, prow): CU row yb + i (i = 0..7)
     auto emit = [&](auto i_c, const s2 (&prow)[4]) {
       constexpr int i = decltype(i_c)::value;
-      if constexpr (i % 4 == 0) orig.load_block(yb + i);
       if constexpr (i < 4) {
         uint32_t d[4];
-        residual_row<i>(prow, orig.template at<i>(yb), d);
+        residual_row<i>(prow, orig(yb + i), d);
 #pragma unroll
         for (int c = 0; c < 4; c++) dA[4 * i + c] = d[c];
       } else {
         uint32_t dB[4];
-        residual_row<i - 4>(prow, orig.template at<i - 4>(yb + 4), dB);
+        residual_row<i - 4>(prow, orig(yb + i), dB);
         if constexpr (ORIG::TR) pair_row_tr<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
         else pair_row<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
       }
