@@ -34,21 +34,16 @@ t0, t1, hw = raw[:, SLOTS - 3].astype(np.int64), raw[:, SLOTS - 2].astype(np.int
 clk = raw[:, :SLOTS - 3].astype(np.int64)
 per_item = clk.sum(axis=1) / 8.0  # 8 waves share an item's tasks
 # placement: HW_ID cu_id bits 11:8, sh 12, se 15:13; XCC_ID low 4 bits of the high word
-cu = ((hw >> 8) & 15) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 7) << 5) | (((hw >> 32) & 15) << 8)
-t0 = t0 - t0.min()
-dur_us = (t1 - raw[:, SLOTS - 3].astype(np.int64)) / 100.0  # s_memrealtime: 100 MHz
 ne = per_item > 0
-print(json.dumps({"launch_span_us": float((t1.max() - raw[:, SLOTS - 3].astype(np.int64).min()) / 100.0),
-                  "item_us_p50_p90_max": [round(float(np.percentile(dur_us[ne], p)), 1) for p in (50, 90, 100)],
-                  "start_us_max": float(t0.max() / 100.0), "distinct_cus": int(len(set(cu.tolist()))),
-                  "items_per_cu_max": int(np.bincount(np.unique(cu, return_inverse=True)[1]).max())}))
-order = np.argsort(-dur_us)[:8]
-print(json.dumps([{"item": int(i), "us": round(float(dur_us[i]), 1), "start_us": round(float(t0[i] / 100.0), 1),
-                   "cu": int(cu[i])} for i in order]))
-busy = per_item[per_item > 0]
-q = np.percentile(busy, [50, 90, 99, 100])
-print(json.dumps({"items": int(n), "nonempty": int(busy.size), "mean_cycles_per_wave": round(float(busy.mean())),
-                  "p50": round(q[0]), "p90": round(q[1]), "p99": round(q[2]), "max": round(q[3]),
-                  "max_over_mean": round(float(q[3] / busy.mean()), 3),
-                  "tasks_per_item_max": int((clk > 0).sum(axis=1).max()),
-                  "max_task_cycles": int(clk.max()), "sorted_top": sorted(busy.round().astype(int).tolist())[-12:]}))
+s0 = raw[:, SLOTS - 3].astype(np.int64)
+t0 = s0[ne].min()
+cu = ((hw >> 8) & 15) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 7) << 5) | (((hw >> 32) & 15) << 8)
+rows = np.stack([np.arange(n)[ne], (s0[ne] - t0), (t1[ne] - t0), cu[ne].astype(np.int64), per_item[ne].astype(np.int64)], 1)
+out = os.environ.get("ITEM_CSV")
+if out:
+    np.savetxt(out, rows, fmt="%d", delimiter=",", header="item,start_10ns,end_10ns,cu,task_cycles_per_wave")
+dur = (rows[:, 2] - rows[:, 1]) / 100.0
+print(json.dumps({"launch_span_us": float(rows[:, 2].max() / 100.0), "last_start_us": float(rows[:, 1].max() / 100.0),
+                  "item_us_p10_p50_p90_max": [round(float(np.percentile(dur, p)), 1) for p in (10, 50, 90, 100)],
+                  "distinct_cus": int(len(set(rows[:, 3].tolist()))),
+                  "max_items_per_cu": int(np.bincount(np.unique(rows[:, 3], return_inverse=True)[1]).max())}))
