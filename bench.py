@@ -246,15 +246,53 @@ def cpu_baseline(width, height, seed, budget_s=10.0):
                       "the C oracle oracle/mip_oracle.c, OpenMP %d threads, %.1f s" % (n, width, height, threads, dt)}
 
 
+def reference_kernel_trace(cmd, frames, reps):
+    """Device time per frame of the reference's kernels from a rocprofv3 kernel trace of
+    ref_runner (its CL profiling timestamps are unusable on this runtime: END precedes
+    START), or None when rocprofv3 is not available."""
+    import csv
+    import shutil
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    d = tempfile.mkdtemp(prefix="refprof_")
+    try:
+        subprocess.run([prof, "--kernel-trace", "--stats", "-d", d, "-o", "ref", "--output-format", "csv", "--"] + cmd,
+                       capture_output=True, timeout=240, check=True, env=dict(os.environ, TMPDIR="/tmp"))
+        stats = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith("kernel_stats.csv")]
+        per = {}
+        for row in csv.DictReader(open(stats[0])):
+            if row["Name"] in ("initBoundaries", "MIP_ReducedPred", "upsampleDistortion") or row["Name"].startswith("filterFrame"):
+                per[row["Name"]] = float(row["TotalDurationNs"]) * 1e-6 / (frames * reps)
+        return per if per else None
+    except Exception:
+        return None
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def reference_gpu(width, height, frames, seed):
     runner = os.path.join(REPO, "oracle", "_ref", "ref_runner")
     if not os.path.exists(runner):
         return None
     try:
-        out = subprocess.run([runner, "--bins", os.path.join(REPO, "oracle", "_ref"), "--width", str(width),
-                              "--height", str(height), "--frames", str(frames), "--synth", "0:%x" % seed,
-                              "--reps", "2"], capture_output=True, timeout=180, check=True).stdout.decode()
+        cmd = [runner, "--bins", os.path.join(REPO, "oracle", "_ref"), "--width", str(width),
+               "--height", str(height), "--frames", str(frames), "--synth", "0:%x" % seed, "--reps", "2"]
+        out = subprocess.run(cmd, capture_output=True, timeout=180, check=True).stdout.decode()
         d = json.loads(out.strip().splitlines()[-1])
+        trace = reference_kernel_trace(cmd, frames, 2)
+        if trace:
+            ms = sum(trace.values())
+            return {"value": round(1000.0 / ms, 3), "unit": "frames/s (device time: rocprofv3 kernel trace of the reference's kernels)",
+                    "kernel_ms_per_frame": {k: round(v, 4) for k, v in trace.items()},
+                    "host_timed_value": round(1000.0 / d["device_ms_per_frame"], 3),
+                    "wall_value": round(1000.0 / d["wall_ms_per_frame"], 2),
+                    "event_fallbacks": int(d.get("event_fallbacks", 0)),
+                    "event_fallback_reason": d.get("event_fallback_reason") or None, "device": d["device"],
+                    "note": "reference intra.cl kernels (initBoundaries, MIP_ReducedPred, 3x upsampleDistortion) "
+                            "compiled by the AMD OpenCL compiler, same GPU, same synthetic frames; host_timed_value: "
+                            "enqueue + clFinish around each kernel (CL profiling events unusable)"}
         if not d["device_ms_per_frame"] > 0:
             return {"error": "no device timing", "raw": d}
         # device time from the CL profiling timestamps of every kernel; a kernel whose
