@@ -9,7 +9,7 @@ import oracle_lib as O
 from mipgpu import FILTERS, layout, unavailable_cus
 from mipgpu.synth import synth_frame
 
-SIZES = [(416, 240), (264, 136), (292, 36), (300, 68), (128, 4), (1280, 720), (256, 136), (832, 480)]
+SIZES = [(416, 240), (264, 136), (292, 36), (300, 68), (128, 4), (1280, 720), (256, 136), (832, 480), (4, 4), (132, 4), (4, 132), (8, 36)]
 
 
 @pytest.mark.parametrize("w,h", SIZES)
