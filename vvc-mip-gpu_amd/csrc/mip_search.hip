@@ -81,6 +81,10 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #ifndef MIP_PAIR_BLOCKS
 #define MIP_PAIR_BLOCKS 1  // classes with an even block count per lane walk block pairs (A/B knob)
 #endif
+#ifndef MIP_PRIO_BALANCE
+#define MIP_PRIO_BALANCE 0  // wave priority follows the item's remaining tasks (A/B knob; measured
+                            // -1.7 % at 384 frames / -1.5 % at 32, 1 frame 0.184 -> 0.177 ms: off)
+#endif
 #ifndef MIP_ONLY_CLASS
 #define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
 #endif
@@ -1560,6 +1564,20 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
         if (lane == 0) tn = atomicAdd(next_task, 1u);
         const int t = (int)__builtin_amdgcn_readfirstlane(tn);
         if (t >= ntasks) break;
+#if MIP_PRIO_BALANCE
+        // Two workgroups share a CU, and the SIMD arbiter serves the older waves first: in a
+        // small launch the first workgroup of a CU finished its item in 98 us while the
+        // second, starved, took 170 us (profiles/r04_item_timeline_1frame.csv).  A wave's
+        // priority follows the share of its item still to do, so the workgroup that is
+        // behind is served first and the two finish together.
+        {
+          const int rem4 = 4 * (ntasks - t);  // uniform
+          if (rem4 > 3 * ntasks) __builtin_amdgcn_s_setprio(3);
+          else if (rem4 > 2 * ntasks) __builtin_amdgcn_s_setprio(2);
+          else if (rem4 > ntasks) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         const uint64_t c0 = clk ? __builtin_readcyclecounter() : 0;
         const WaveTask task = a.tasks[tbase + t];
         switch (task.cls) {
