@@ -36,14 +36,16 @@ def run(eng, n, reps=40):
 
 print(json.dumps({"build_id": build_id(), "size": [W, H]}), flush=True)
 # SB_CUTS: task cut factors to try (MIPGPU_CUT_FACTOR, engine creation); SB_ORDERS: 1 = LPT, 0 = raster
-for cut in os.environ.get("SB_CUTS", "2").split(","):
+for cut, hp in [(c, h) for c in os.environ.get("SB_CUTS", "2").split(",") for h in os.environ.get("SB_HELP", "1").split(",")]:
     os.environ["MIPGPU_CUT_FACTOR"] = cut
+    os.environ["MIPGPU_HELP"] = hp
     for order in os.environ.get("SB_ORDERS", "1,0").split(","):
         os.environ["MIPGPU_ORDER"] = order
         for sl in map(int, os.environ.get("SB_SLICES", "0,1,2,4").split(",")):
             eng = MipEngine(W, H, max_batch=max(NF), slices_per_ctu=sl)
             res = {n: round(run(eng, n), 4) for n in NF}
             eng.close()
-            print(json.dumps({"cut": float(cut), "order": "lpt" if order == "1" else "raster", "slices": sl or "auto",
+            print(json.dumps({"cut": float(cut), "help": hp == "1", "order": "lpt" if order == "1" else "raster",
+                              "slices": sl or "auto",
                               "ms_per_launch": res,
                               "frames_per_s": {n: round(n / (ms * 1e-3), 1) for n, ms in res.items()}}), flush=True)

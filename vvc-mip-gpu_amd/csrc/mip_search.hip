@@ -85,6 +85,9 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #define MIP_PRIO_BALANCE 0  // wave priority follows the item's remaining tasks (A/B knob; measured
                             // -1.7 % at 384 frames / -1.5 % at 32, 1 frame 0.184 -> 0.177 ms: off)
 #endif
+#ifndef MIP_HELP_MIN_TASKS
+#define MIP_HELP_MIN_TASKS 2  // help mode: tasks an item must have left to be joined (A/B knob)
+#endif
 #ifndef MIP_ONLY_CLASS
 #define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
 #endif
@@ -1471,6 +1474,24 @@ __device__ __forceinline__ bool far_from_end(const SearchArgs &a, uint32_t item)
 }
 constexpr uint32_t kTakeItem = 0xffffffffu;  // "take the next item after this one" (PF)
 
+// Help mode (SearchArgs::task_ctr): the item queue is empty -- the next item in progress with
+// at least two tasks left, in queue order (each item is examined by one helper: a monotonic
+// cursor), or nitems.  One thread of the workgroup.  In a small launch the two workgroups
+// of a CU progress at very different rates (the SIMD arbiter serves the older waves first:
+// 98 vs 170 us for the two items of a CU in a 1080p frame, profiles/r04_item_timeline_1frame.csv),
+// so the first to finish joins the other's item instead of idling.
+__device__ __forceinline__ uint32_t take_help(const SearchArgs &a) {
+  for (;;) {
+    const uint32_t j = atomicAdd(a.queue + kHelpCursor, 1u);
+    if (j >= a.nitems) return a.nitems;
+    const ItemPos p(a, j);
+    const int l = (a.ctu_var[p.ctu] * 4 + p.quad) * a.slices + p.slice;
+    const uint32_t nt = (uint32_t)(a.list_begin[l + 1] - a.list_begin[l]);
+    if (__hip_atomic_load(a.task_ctr + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + MIP_HELP_MIN_TASKS <= nt) return j;
+  }
+}
+
+
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
 template <bool ALT, bool DEC, bool PF_>
 __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
@@ -1495,8 +1516,17 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   // (PF: the first item is taken like a late one, by the loop)
   if (threadIdx.x < kCounterWords) counters[threadIdx.x] = threadIdx.x == 2 && PF ? kTakeItem : 0u;
   __syncthreads();
+  // help mode (small launches): counters[9] = 1 while the workgroup helps another's item
+  const bool help = !PF && a.task_ctr != nullptr;
   if (!PF) {
-    if (threadIdx.x == 0) counters[2] = take_item(a, counters + 8);
+    if (threadIdx.x == 0) {
+      uint32_t it = take_item(a, counters + 8);
+      if (help && it >= a.nitems) {
+        it = take_help(a);
+        counters[9] = 1;
+      }
+      counters[2] = it;
+    }
     __syncthreads();
   }
   int par = 0;          // workgroup-uniform: parity of the item (window buffer, counter set)
@@ -1519,9 +1549,12 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     const int tbase = a.list_begin[list], ntasks = a.list_begin[list + 1] - tbase;
     uint16_t *org = org_buf + (PF ? par * kTileElems : 0);
     uint16_t *ref = ALT ? lattice : org;
+    const bool helping = help && counters[9] != 0;  // workgroup-uniform: another's item
 
     // CUs whose cost the reference leaves undefined (edge CTUs): MIP_COST_UNAVAILABLE, no search
-    if (DEC) {
+    // (by the item's own workgroup)
+    if (helping) {
+    } else if (DEC) {
       const size_t gbase = ((size_t)frame * a.nctus + ctu) * MIP_CUS_PER_CTU;
       const int f0 = a.dfill_begin[vq], nf = a.dfill_begin[vq + 1] - f0;
       for (int i = slice * blockDim.x + threadIdx.x; i < nf; i += a.slices * blockDim.x) {
@@ -1554,14 +1587,14 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
       uint64_t *clk = a.wave_clock ? a.wave_clock + (size_t)item * kClockSlots : nullptr;
       // profiling: item start / end (s_memrealtime, 100 MHz) and the workgroup's place
       // (HW_ID: CU / SIMD / SE; XCC_ID) in the last three slots
-      if (clk && threadIdx.x == 0) {
+      if (clk && threadIdx.x == 0 && !helping) {
         clk[kClockSlots - 3] = __builtin_amdgcn_s_memrealtime();
         clk[kClockSlots - 1] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                                (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
       }
       for (;;) {
         uint32_t tn = 0;
-        if (lane == 0) tn = atomicAdd(next_task, 1u);
+        if (lane == 0) tn = help ? atomicAdd(a.task_ctr + item, 1u) : atomicAdd(next_task, 1u);
         const int t = (int)__builtin_amdgcn_readfirstlane(tn);
         if (t >= ntasks) break;
 #if MIP_PRIO_BALANCE
@@ -1662,7 +1695,12 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
       __syncthreads();  // every wave is done with the window and the item's counters
       if (threadIdx.x == 0) {
         next_task[0] = 0;
-        next_task[2] = take_item(a, counters + 8);
+        uint32_t it = counters[9] ? a.nitems : take_item(a, counters + 8);
+        if (help && it >= a.nitems) {
+          it = take_help(a);
+          counters[9] = 1;
+        }
+        next_task[2] = it;
       }
       __syncthreads();  // the next item is in place
     }
@@ -1670,12 +1708,21 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   }
   // The last workgroup to leave resets the queue's counters for the next launch that uses it
   // (the host never runs two launches on one pair at the same time).
+  // Help mode: the per-item task counters too (every workgroup has left, none touches them).
   if (threadIdx.x == 0) {
     __threadfence();
-    if (atomicAdd(a.queue + kQueueChunks, 1u) == gridDim.x - 1) {
+    const bool last = atomicAdd(a.queue + kQueueChunks, 1u) == gridDim.x - 1;
+    if (last) {
       for (int c = 0; c < kQueueChunks; c++) atomicExch(a.queue + c, 0u);
+      atomicExch(a.queue + kHelpCursor, 0u);
       atomicExch(a.queue + kQueueChunks, 0u);
     }
+    counters[10] = last;
+  }
+  if (help) {
+    __syncthreads();
+    if (counters[10])
+      for (uint32_t i = threadIdx.x; i < a.nitems; i += blockDim.x) atomicExch(a.task_ctr + i, 0u);
   }
 }
 
@@ -1794,6 +1841,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const bool dec = a.cost == nullptr;
   if (dec && (!a.best_cost || !a.dfill_begin)) return hipErrorInvalidValue;
   const bool pf = !alt_refs && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
+  if (pf || a.chunks > 1 || a.nitems > a.help_cap) a.task_ctr = nullptr;  // help mode: small launches only
   const size_t lds = search_lds_bytes(alt_refs, pf);
   const dim3 grid(groups), block(64 * kWaves);
   if (alt_refs) {

@@ -539,6 +539,10 @@ struct mip_engine {
   // launches on different streams never share one.
   static constexpr int kQueueSlots = 16;
   uint32_t *d_queue = nullptr;
+  // help mode of small launches (SearchArgs::task_ctr): per-item task counters, help_cap
+  // words per queue slot (a slot's counters are used by the launch that holds the slot)
+  uint32_t *d_task_ctr = nullptr;
+  uint32_t help_cap = 0;
   hipEvent_t queue_done[kQueueSlots] = {};
   struct QueueOps {
     mip_engine *e;
@@ -567,6 +571,11 @@ constexpr int kSmallLaunchItemsPerGroup = 32;
 // Per-item cost beyond its tasks (window staging, barriers, fills), in the task cost
 // model's units (pair_cost: VALU instructions per lane).
 constexpr double kItemOverhead = 600.0;
+
+bool help_enabled() {
+  const char *e = getenv("MIPGPU_HELP");  // A/B knob: 0 = no helping in small launches
+  return !(e && *e == '0');
+}
 
 bool lpt_order_enabled() {
   const char *e = getenv("MIPGPU_ORDER");  // A/B knob: 0 = raster item order in small launches
@@ -721,6 +730,7 @@ int mip_engine_destroy(mip_engine *e) {
     if (e->d_fixup[m]) (void)hipFree(e->d_fixup[m]);
   }
   if (e->d_queue) (void)hipFree(e->d_queue);
+  if (e->d_task_ctr) (void)hipFree(e->d_task_ctr);
   if (e->h_status) (void)hipHostFree(e->h_status);
   for (hipEvent_t ev : e->queue_done)
     if (ev) (void)hipEventDestroy(ev);
@@ -821,6 +831,10 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   for (int alt = 0; alt < 2; alt++)
     if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0)) < 1)
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
+  e->help_cap = (uint32_t)kSmallLaunchItemsPerGroup * (uint32_t)std::max(e->resident[0], e->resident[1]);
+  ALLOC(e->d_task_ctr, (size_t)e->help_cap * mip_engine::kQueueSlots * sizeof(uint32_t));
+  if (hipMemset(e->d_task_ctr, 0, (size_t)e->help_cap * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
+    return cleanup(fail("hipMemset failed"));
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
   const CtuVariants cv = ctu_variants(width, height, o.filter);
   if (cv.pattern.size() > (size_t)mipgpu::kMaxCtuVariants)
@@ -1021,6 +1035,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const int slot = e->queue.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + mipgpu::kQueueWords * slot;
+  a.task_ctr = help_enabled() ? e->d_task_ctr + (size_t)e->help_cap * slot : nullptr;  // launch_search keeps
+  a.help_cap = e->help_cap;                                                            // it for small launches
   const hipError_t le = mipgpu::launch_search(a, nframes, alt, e->resident[alt ? 1 : 0], s);
   if (le != hipSuccess) {
     e->queue.failed(slot);  // the pair is cleared before its next use
