@@ -178,6 +178,9 @@ def valu_section(pmc, kernel_ms, alg_ops):
     if insts:
         rate = insts / (kernel_ms * 1e-3)
         out["achieved"], out["frac"] = round(rate / 1e9, 1), round(rate / VALU_PEAK_INSTS, 4)
+        # against the two-per-quad-cycle ceiling (dual issue: both eligible, from two waves)
+        out["dual_peak"] = round(2 * VALU_PEAK_INSTS / 1e9, 1)
+        out["frac_of_dual_peak"] = round(rate / (2 * VALU_PEAK_INSTS), 4)
     flops = pmc.get("mfma_f16_flops_per_launch")
     if flops:
         # phase A (the MIP matrix products) on the matrix cores: f16 MFMA rate vs the dense peak
