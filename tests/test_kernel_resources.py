@@ -3,8 +3,9 @@ objects' metadata, tests/kernel_resources.py).
 
 * No kernel spills to scratch (an out-of-line device helper in the search loop once cost
   192 bytes per lane of scratch, 12 % of the search time and 2x its HBM traffic).
-* mip_search_kernel: <= 128 VGPRs, i.e. 4 waves per SIMD -- two 8-wave workgroups per CU,
-  the occupancy the persistent grid is sized for.
+* mip_search_kernel: <= 128 VGPRs, i.e. 4 waves per SIMD -- two 8-wave workgroups per CU
+  (or one 16-wave workgroup in small launches), the occupancy the persistent grid is sized
+  for.
 * filter_kernel: <= 64 VGPRs (8 waves per SIMD).
 """
 import os
@@ -30,7 +31,9 @@ def _named(kernels, part):
 
 
 def test_every_kernel_variant_present(kernels):
-    assert len(_named(kernels, "mip_search_kernel")) == 6  # {orig, alt} x {table, decisions} x prefetch (orig)
+    # {orig, alt} x {table, decisions} x prefetch (orig), and the 16-wave variants of small
+    # launches ({orig, alt} x {table, decisions}, no prefetch)
+    assert len(_named(kernels, "mip_search_kernel")) == 10
     assert len(_named(kernels, "filter_kernel")) == 8      # radius x int/float x 2-D/separable
     for part in ("fixup_kernel", "best_mode_kernel", "dec_split_kernel"):
         _named(kernels, part)

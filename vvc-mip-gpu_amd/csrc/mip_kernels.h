@@ -173,11 +173,14 @@ struct FilterArgs {
   int kernel_idx;
 };
 
-int search_waves_per_group();
+// Waves per search workgroup: two 8-wave workgroups share a CU in batched launches; small
+// launches can run one 16-wave workgroup per CU instead ("wide"), whose waves share one
+// item's tasks (launch_search).
+constexpr int kSearchWaves = 8, kWideWaves = 16;
 // Workgroups of the search kernel resident on the current device at once (persistent grid
 // size); computed once per engine (mip_engine_create), 0 on error.
-int search_resident_groups(bool alt_refs);
-hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, hipStream_t s);
+int search_resident_groups(bool alt_refs, bool wide);
+hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s);
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 // Decisions only, CUs whose mode pairs are cut over several tasks (split CUs of the CTU's
 // variant: [split_begin[v], split_begin[v+1]) of `split`, at most max_split per variant):

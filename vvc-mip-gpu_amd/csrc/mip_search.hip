@@ -92,7 +92,6 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
 #endif
 
-constexpr int kWaves = 8;        // waves per workgroup
 constexpr int kPitch = 68;       // LDS row pitch in samples (34 dwords: conflict-free rows)
 constexpr int kColOff = 4;       // LDS column of quadrant column 0 (-4..-1: left halo)
 constexpr int kTileElems = (65 * kPitch + 7) / 8 * 8;  // quadrant rows -1..63
@@ -1332,7 +1331,7 @@ struct WindowStager {
   }
 };
 
-// (whole workgroup, kWaves * 64 threads: every thread's loads are issued before its first
+// (whole workgroup, NT threads: every thread's loads are issued before its first
 // LDS store, so the workgroup waits for HBM once, not once per load)
 // Input contract: a staged sample above 10 bits (any of bits 10..15 of the OR of the
 // loaded chunks) marks the search's status word (SearchArgs::status); the costs of such a
@@ -1342,10 +1341,11 @@ __device__ __forceinline__ void flag_above_10_bits(uint32_t bits, uint32_t *stat
   if (bits & kAbove10Bits) status[word] = 1u;
 }
 
+template <int NT>
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
                                            int x0, int y0, uint32_t *status) {
-  const WindowStager<64 * kWaves> st(frame, width, height, x0, y0, (int)threadIdx.x);
-  constexpr int N = WindowStager<64 * kWaves>::N;
+  const WindowStager<NT> st(frame, width, height, x0, y0, (int)threadIdx.x);
+  constexpr int N = WindowStager<NT>::N;
   uint2 v[N];
 #pragma unroll
   for (int k = 0; k < N; k++)
@@ -1387,10 +1387,11 @@ struct ItemPos {
 // by linear index like the window (frame_chunk).
 // check: caller-supplied references (SearchArgs::check_refs) must be 10-bit too, except frame
 // columns W-2, W-1, whose CUs the exact fixup kernel searches (mipgpu.cpp reads_last_columns).
+template <int NT>
 __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
                                               int x0, int y0, bool check, uint32_t *status) {
   // all loads first, then all LDS stores (as stage_tile)
-  constexpr int NT = 64 * kWaves, kChunks = kPitch / 4, NR = 16 * kChunks, NC = 16 * 65;
+  constexpr int kChunks = kPitch / 4, NR = 16 * kChunks, NC = 16 * 65;
   constexpr int NRL = (NR + NT - 1) / NT, NCL = (NC + NT - 1) / NT;
   uint2 rv[NRL];
   uint16_t cv[NCL];
@@ -1493,8 +1494,9 @@ __device__ __forceinline__ uint32_t take_help(const SearchArgs &a) {
 
 
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
-template <bool ALT, bool DEC, bool PF_>
-__global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a) {
+// NW: waves per workgroup (kSearchWaves; kWideWaves for small launches, one workgroup per CU)
+template <bool ALT, bool DEC, bool PF_, int NW>
+__global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = PF_ && !ALT;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles<ALT, PF> windows
@@ -1502,7 +1504,7 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
   uint8_t *w = smem + (kOrgTiles<ALT, PF> * kTileElems + (ALT ? kLatElems : 0)) * 2;
   uint8_t *zero = w + kTableBytes;
   uint8_t *waves = zero + kZeroBytes;
-  uint32_t *counters = reinterpret_cast<uint32_t *>(waves + kWaves * kWaveBytes);
+  uint32_t *counters = reinterpret_cast<uint32_t *>(waves + NW * kWaveBytes);
 
   for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(w)[i] = a.tables[i];
@@ -1575,8 +1577,8 @@ __global__ __launch_bounds__(64 * kWaves, 4) void mip_search_kernel(SearchArgs a
     }
     if (ntasks > 0) {  // workgroup-uniform
       if (!PF || !staged) {
-        stage_tile(org, a.orig + fofs, a.width, a.height, fx0, fy0, a.status);
-        if (ALT) stage_lattice(ref, a.refs + fofs, a.width, a.height, fx0, fy0, a.check_refs != 0, a.status);
+        stage_tile<64 * NW>(org, a.orig + fofs, a.width, a.height, fx0, fy0, a.status);
+        if (ALT) stage_lattice<64 * NW>(ref, a.refs + fofs, a.width, a.height, fx0, fy0, a.check_refs != 0, a.status);
         __syncthreads();
       }
 
@@ -1795,32 +1797,36 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
 
 }  // namespace
 
-int search_waves_per_group() { return kWaves; }
-
-size_t search_lds_bytes(bool alt, bool pf) {
+size_t search_lds_bytes(bool alt, bool pf, int waves) {
   return (size_t)((pf && !alt ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
-         (size_t)kWaves * kWaveBytes + kCounterWords * 4;
+         (size_t)waves * kWaveBytes + kCounterWords * 4;
 }
 
-template <bool ALT, bool DEC, bool PF>
+template <bool ALT, bool DEC, bool PF, int NW>
 static int resident_per_cu() {
   int per_cu = 0;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<ALT, DEC, PF>, 64 * kWaves,
-                                                      search_lds_bytes(ALT, PF)) == hipSuccess ? per_cu : 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mip_search_kernel<ALT, DEC, PF, NW>, 64 * NW,
+                                                      search_lds_bytes(ALT, PF, NW)) == hipSuccess ? per_cu : 0;
 }
 
-int search_resident_groups(bool alt) {
+int search_resident_groups(bool alt, bool wide) {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  // every variant of the kernel shares the grid size
-  const int per_cu = alt ? std::min(resident_per_cu<true, false, false>(), resident_per_cu<true, true, false>())
-                         : std::min({resident_per_cu<false, false, false>(), resident_per_cu<false, true, false>(),
-                                     resident_per_cu<false, false, true>(), resident_per_cu<false, true, true>()});
+  // every variant of a width shares the grid size
+  constexpr int S = kSearchWaves, L = kWideWaves;
+  int per_cu;
+  if (wide)
+    per_cu = alt ? std::min(resident_per_cu<true, false, false, L>(), resident_per_cu<true, true, false, L>())
+                 : std::min(resident_per_cu<false, false, false, L>(), resident_per_cu<false, true, false, L>());
+  else
+    per_cu = alt ? std::min(resident_per_cu<true, false, false, S>(), resident_per_cu<true, true, false, S>())
+                 : std::min({resident_per_cu<false, false, false, S>(), resident_per_cu<false, true, false, S>(),
+                             resident_per_cu<false, false, true, S>(), resident_per_cu<false, true, true, S>()});
   return per_cu >= 1 ? cus * per_cu : 0;
 }
 
-hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, hipStream_t s) {
+hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s) {
   if (args.slices < 1 || !args.queue || !args.status || resident < 1) return hipErrorInvalidValue;
   SearchArgs a = args;
   if (a.ctu0 < 0 || a.nrange < 1 || a.ctu0 + a.nrange > a.nctus) return hipErrorInvalidValue;
@@ -1840,19 +1846,32 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;
   if (dec && (!a.best_cost || !a.dfill_begin)) return hipErrorInvalidValue;
-  const bool pf = !alt_refs && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
+  const bool pf = !alt_refs && !wide && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
   if (pf || a.chunks > 1 || a.nitems > a.help_cap) a.task_ctr = nullptr;  // help mode: small launches only
-  const size_t lds = search_lds_bytes(alt_refs, pf);
-  const dim3 grid(groups), block(64 * kWaves);
+  const size_t lds = search_lds_bytes(alt_refs, pf, wide ? kWideWaves : kSearchWaves);
+  const dim3 grid(groups);
+  constexpr int S = kSearchWaves, L = kWideWaves;
+  if (wide) {
+    const dim3 block(64 * L);
+    if (alt_refs) {
+      if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true, false, L>), grid, block, lds, s, a);
+      else hipLaunchKernelGGL((mip_search_kernel<true, false, false, L>), grid, block, lds, s, a);
+    } else {
+      if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, false, L>), grid, block, lds, s, a);
+      else hipLaunchKernelGGL((mip_search_kernel<false, false, false, L>), grid, block, lds, s, a);
+    }
+    return hipGetLastError();
+  }
+  const dim3 block(64 * S);
   if (alt_refs) {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true, false>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<true, false, false>), grid, block, lds, s, a);
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true, false, S>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<true, false, false, S>), grid, block, lds, s, a);
   } else if (pf) {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, true>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<false, false, true>), grid, block, lds, s, a);
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, true, S>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<false, false, true, S>), grid, block, lds, s, a);
   } else {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, false>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<false, false, false>), grid, block, lds, s, a);
+    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, false, S>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((mip_search_kernel<false, false, false, S>), grid, block, lds, s, a);
   }
   return hipGetLastError();
 }

@@ -506,6 +506,7 @@ struct mip_engine {
   // more, smaller workgroups to fill the chip (see pick_work).
   struct Work {
     int slices = 1;
+    bool wide = false;  // lists for one 16-wave workgroup per CU (small launches, pick_work)
     mipgpu::WaveTask *d_tasks = nullptr;
     mipgpu::Job *d_jobs = nullptr;
     int *d_lists = nullptr;
@@ -520,14 +521,15 @@ struct mip_engine {
     std::vector<double> order_cost;
   };
   std::vector<Work> work;
-  // pick_work's choice per frame count for small launches (slice count index into `work`)
-  std::vector<int> small_choice;
+  // pick_work's choice per frame count for small launches (index into `work`), [wide]
+  std::vector<int> small_choice[2];
   uint8_t *d_tables = nullptr;
   uint8_t *d_ctu_var[kMaps] = {};           // [map][nctus] CTU variant (ctu_variants: orig /
                                             // caller refs / engine-filtered refs)
   mipgpu::FixupCu *d_fixup[kMaps] = {};     // alt refs: CUs of the exact per-CU kernel, per map
   int nfixup[kMaps] = {};
   int resident[2] = {0, 0};  // persistent search grid (workgroups resident on this device), [alt]
+  int resident_wide[2] = {0, 0};  // the same for 16-wave workgroups
   // Engine-owned reference scratch d_refs, written by the engine filter when a device-API
   // search has no caller references: every such search records refs_done on its stream, and
   // the next writer of d_refs (another device-API search, on any stream, or a host-API call)
@@ -573,8 +575,12 @@ constexpr int kSmallLaunchItemsPerGroup = 32;
 constexpr double kItemOverhead = 600.0;
 
 bool help_enabled() {
-  const char *e = getenv("MIPGPU_HELP");  // A/B knob: 0 = no helping in small launches
-  return !(e && *e == '0');
+  // A/B knob, off by default: 1 = workgroups join items in progress in small launches
+  // (measured: 1 frame 0.188 -> 0.185 ms, 2-16 frames 3-4 % slower: the per-task global
+  // atomics cost more than the helping gains, since a slow item's tasks are mostly claimed
+  // by the time its neighbour finishes; profiles/r04_small_batch_help.jsonl)
+  const char *e = getenv("MIPGPU_HELP");
+  return e && *e == '1';
 }
 
 bool lpt_order_enabled() {
@@ -595,27 +601,46 @@ double lpt_makespan(const std::vector<double> &order_cost, int nframes, int grou
   return *std::max_element(fin.begin(), fin.end());
 }
 
-// Slice count for a launch of `nframes`: items (quadrant x slice) for the persistent grid.
+// Small launches on 16-wave workgroups, one per CU (MIPGPU_WIDE: 0 = never, 1 = every small
+// launch; default: below kWideItemsPerGroup items per CU at one slice).  Two 8-wave workgroups
+// on a CU progress at very different rates when both run an item (the SIMD arbiter serves the
+// older waves first: 98 vs 170 us for the two items of a CU in a 1080p frame,
+// profiles/r04_item_timeline_1frame.csv), so a launch of ~2 items per CU ends with one
+// workgroup running alone; one wide workgroup per CU has all 16 waves on one item's tasks.
+constexpr int kWideItemsPerGroup = 8;
+bool wide_launch(long long items1, int cus) {
+  const char *e = getenv("MIPGPU_WIDE");
+  if (e && *e == '0') return false;
+  if (e && *e == '1') return true;
+  return items1 < (long long)kWideItemsPerGroup * cus;
+}
+
+// Work lists for a launch of `nframes`: items (quadrant x slice) for the persistent grid.
 // Large launches (>= kSmallLaunchItemsPerGroup items per workgroup at one slice): one slice.
-// Small ones take their items longest first; the slice count is the one whose predicted
-// makespan (lpt_makespan, per frame count, cached) is the shortest.  (Before the LPT order:
-// 1 frame -> 2 slices 5076 frames/s at 1080p (1: 4842, 4: 4770).)
-const mip_engine::Work &pick_work(mip_engine *e, int nframes, int nrange, int groups) {
+// Small ones take their items longest first, on 8- or 16-wave workgroups (wide_launch); the
+// slice count is the one whose predicted makespan (lpt_makespan, per frame count, cached) is
+// the shortest.  (Before the LPT order: 1 frame -> 2 slices 5076 frames/s at 1080p (1: 4842,
+// 4: 4770).)
+const mip_engine::Work &pick_work(mip_engine *e, int nframes, int nrange, bool alt) {
+  const int groups = e->resident[alt ? 1 : 0];
   const long long items1 = 4LL * nrange * nframes;  // items at one slice
-  if (e->work.size() == 1) return e->work[0];
   if (nrange != e->nctus || items1 >= (long long)kSmallLaunchItemsPerGroup * groups || !lpt_order_enabled()) {
     const int want = items1 < 1000 && nrange != e->nctus ? 2 : 1;
-    const mip_engine::Work *best = &e->work[0];
+    const mip_engine::Work *best = nullptr;
     for (const mip_engine::Work &w : e->work)
-      if (std::abs(w.slices - want) < std::abs(best->slices - want)) best = &w;
+      if (!w.wide && (!best || std::abs(w.slices - want) < std::abs(best->slices - want))) best = &w;
     return *best;
   }
-  if ((int)e->small_choice.size() <= nframes) e->small_choice.resize(nframes + 1, -1);
-  int &ch = e->small_choice[nframes];
+  const bool wide = wide_launch(items1, e->resident_wide[alt ? 1 : 0]);
+  std::vector<int> &cache = e->small_choice[wide ? 1 : 0];
+  if ((int)cache.size() <= nframes) cache.resize(nframes + 1, -1);
+  int &ch = cache[nframes];
   if (ch < 0) {
+    const int g = wide ? e->resident_wide[alt ? 1 : 0] : groups;
     double best = 0;
     for (size_t i = 0; i < e->work.size(); i++) {
-      const double m = lpt_makespan(e->work[i].order_cost, nframes, groups);
+      if (e->work[i].wide != wide) continue;
+      const double m = lpt_makespan(e->work[i].order_cost, nframes, g);
       if (ch < 0 || m < best) ch = (int)i, best = m;
     }
   }
@@ -829,7 +854,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   if (hipEventCreateWithFlags(&e->refs_done, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail("hipEventCreate failed"));
   for (int alt = 0; alt < 2; alt++)
-    if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0)) < 1)
+    if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0, false)) < 1 ||
+        (e->resident_wide[alt] = mipgpu::search_resident_groups(alt != 0, true)) < 1)
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
   e->help_cap = (uint32_t)kSmallLaunchItemsPerGroup * (uint32_t)std::max(e->resident[0], e->resident[1]);
   ALLOC(e->d_task_ctr, (size_t)e->help_cap * mip_engine::kQueueSlots * sizeof(uint32_t));
@@ -854,10 +880,14 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   std::vector<int> slice_set;
   if (o.slices_per_ctu > 0) slice_set = {o.slices_per_ctu};
   else slice_set = {1, 2, 4};
-  for (int sl : slice_set) {
-    const WorkLists wl = build_work(sl, mipgpu::search_waves_per_group(), width, height, cv);
+  std::vector<std::pair<int, bool>> work_set;  // (slices, wide)
+  for (int wide = 0; wide < 2; wide++)
+    for (int sl : slice_set) work_set.push_back({sl, wide != 0});
+  for (const auto &[sl, wide] : work_set) {
+    const WorkLists wl = build_work(sl, wide ? mipgpu::kWideWaves : mipgpu::kSearchWaves, width, height, cv);
     mip_engine::Work w;
     w.slices = sl;
+    w.wide = wide;
     e->work.push_back(w);
     mip_engine::Work &ew = e->work.back();
     ALLOC(ew.d_tasks, std::max<size_t>(1, wl.tasks.size()) * sizeof(mipgpu::WaveTask));
@@ -981,7 +1011,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.best_cost = decisions_only ? d_best_cost : nullptr;
   a.sad = d_sad;
   a.satd = d_satd;
-  const mip_engine::Work &work = pick_work(e, nframes, nrange, e->resident[alt ? 1 : 0]);
+  const mip_engine::Work &work = pick_work(e, nframes, nrange, alt);
+  const int resident = work.wide ? e->resident_wide[alt ? 1 : 0] : e->resident[alt ? 1 : 0];
   a.tasks = work.d_tasks;
   a.jobs = work.d_jobs;
   a.list_begin = work.d_lists;
@@ -1016,7 +1047,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     clocks.resize(n);
     static std::atomic<bool> dumped{false};
     if (!dumped.exchange(true)) {
-      const WorkLists wl = build_work(work.slices, mipgpu::search_waves_per_group(), e->width, e->height,
+      const WorkLists wl = build_work(work.slices, work.wide ? mipgpu::kWideWaves : mipgpu::kSearchWaves, e->width, e->height,
                                       ctu_variants(e->width, e->height, e->opts.filter));
       if (FILE *f = fopen((std::string(timing) + ".tasks").c_str(), "w")) {
         fprintf(f, "{\"slices\": %d, \"list_begin\": [", work.slices);
@@ -1037,7 +1068,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.queue = e->d_queue + mipgpu::kQueueWords * slot;
   a.task_ctr = help_enabled() ? e->d_task_ctr + (size_t)e->help_cap * slot : nullptr;  // launch_search keeps
   a.help_cap = e->help_cap;                                                            // it for small launches
-  const hipError_t le = mipgpu::launch_search(a, nframes, alt, e->resident[alt ? 1 : 0], s);
+  const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, s);
   if (le != hipSuccess) {
     e->queue.failed(slot);  // the pair is cleared before its next use
     return fail("search launch failed: %s", hipGetErrorString(le));
