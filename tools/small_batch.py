@@ -36,15 +36,13 @@ def run(eng, n, reps=40):
 
 
 print(json.dumps({"build_id": build_id(), "size": [W, H]}), flush=True)
-# SB_CUTS: task cut factors to try (MIPGPU_CUT_FACTOR, engine creation); SB_HELP: help mode
-# (MIPGPU_HELP); SB_WIDE: 16-wave workgroups (MIPGPU_WIDE: 0 never, 1 every small launch, "auto"
+# SB_CUTS: task cut factors to try (MIPGPU_CUT_FACTOR, engine creation); SB_WIDE: 16-wave workgroups (MIPGPU_WIDE: 0 never, 1 every small launch, "auto"
 # the engine's rule); SB_ORDERS: 1 = LPT, 0 = raster; SB_SLICES: 0 = the engine's choice
-grid = itertools.product(os.environ.get("SB_CUTS", "2").split(","), os.environ.get("SB_HELP", "0").split(","),
+grid = itertools.product(os.environ.get("SB_CUTS", "2").split(","),
                          os.environ.get("SB_WIDE", "auto").split(","), os.environ.get("SB_ORDERS", "1,0").split(","),
                          map(int, os.environ.get("SB_SLICES", "0,1,2,4").split(",")))
-for cut, hp, wide, order, sl in grid:
+for cut, wide, order, sl in grid:
     os.environ["MIPGPU_CUT_FACTOR"] = cut
-    os.environ["MIPGPU_HELP"] = hp
     os.environ["MIPGPU_ORDER"] = order
     if wide == "auto":
         os.environ.pop("MIPGPU_WIDE", None)
@@ -53,7 +51,7 @@ for cut, hp, wide, order, sl in grid:
     eng = MipEngine(W, H, max_batch=max(NF), slices_per_ctu=sl)
     res = {n: round(run(eng, n), 4) for n in NF}
     eng.close()
-    print(json.dumps({"cut": float(cut), "help": hp == "1", "wide": wide, "order": "lpt" if order == "1" else "raster",
+    print(json.dumps({"cut": float(cut), "wide": wide, "order": "lpt" if order == "1" else "raster",
                       "slices": sl or "auto",
                       "ms_per_launch": res,
                       "frames_per_s": {n: round(n / (ms * 1e-3), 1) for n, ms in res.items()}}), flush=True)

@@ -96,14 +96,6 @@ struct SearchArgs {
   // q % nframes.  Null: raster order (frame-major).  Whole-frame launches only.
   const uint32_t *order;
   uint32_t nframes;
-  // Small launches (one queue chunk, no prefetch): the item's tasks are taken from a global
-  // counter per item, task_ctr[item] (zero at launch; the kernel leaves them zero), so that a
-  // workgroup that finds the item queue empty can help an item still in progress (a
-  // workgroup stages the item's window itself and takes tasks from its counter).  Null: tasks
-  // from the workgroup's LDS counter.  help_cap: counters available (launch_search drops the
-  // help mode above it).
-  uint32_t *task_ctr;
-  uint32_t help_cap;
   uint32_t chunks;        // queue chunks, 1..kQueueChunks (set by launch_search)
   uint64_t *wave_clock;   // profiling (MIPGPU_WAVE_TIMING): [workgroup][kClockSlots] cycles per
                           // task of the workgroup's list; else null
@@ -121,8 +113,7 @@ constexpr int kClockSlots = 128;
 // XCD (workgroups b and b + 8 share an XCD), each with its own counter (mip_search.hip
 // take_item).
 constexpr int kQueueChunks = 8;
-constexpr int kQueueWords = 16;  // 8 chunk counters, the done counter, the help cursor, padding to 64 bytes
-constexpr int kHelpCursor = kQueueChunks + 1;  // next item a helping workgroup examines (help mode)
+constexpr int kQueueWords = 16;  // 8 chunk counters, the done counter, padding to 64 bytes
 // CTU variants (mipgpu.cpp ctu_variants): CTUs with the same set of defined CUs share work /
 // fill lists; the lists omit the CUs whose cost the reference leaves undefined.
 constexpr int kMaxCtuVariants = 255;

@@ -541,10 +541,6 @@ struct mip_engine {
   // launches on different streams never share one.
   static constexpr int kQueueSlots = 16;
   uint32_t *d_queue = nullptr;
-  // help mode of small launches (SearchArgs::task_ctr): per-item task counters, help_cap
-  // words per queue slot (a slot's counters are used by the launch that holds the slot)
-  uint32_t *d_task_ctr = nullptr;
-  uint32_t help_cap = 0;
   hipEvent_t queue_done[kQueueSlots] = {};
   struct QueueOps {
     mip_engine *e;
@@ -574,15 +570,6 @@ constexpr int kSmallLaunchItemsPerGroup = 32;
 // model's units (pair_cost: VALU instructions per lane).
 constexpr double kItemOverhead = 600.0;
 
-bool help_enabled() {
-  // A/B knob, off by default: 1 = workgroups join items in progress in small launches
-  // (measured: 1 frame 0.188 -> 0.185 ms, 2-16 frames 3-4 % slower: the per-task global
-  // atomics cost more than the helping gains, since a slow item's tasks are mostly claimed
-  // by the time its neighbour finishes; profiles/r04_small_batch_help.jsonl)
-  const char *e = getenv("MIPGPU_HELP");
-  return e && *e == '1';
-}
-
 bool lpt_order_enabled() {
   const char *e = getenv("MIPGPU_ORDER");  // A/B knob: 0 = raster item order in small launches
   return !(e && *e == '0');
@@ -601,13 +588,29 @@ double lpt_makespan(const std::vector<double> &order_cost, int nframes, int grou
   return *std::max_element(fin.begin(), fin.end());
 }
 
-// Small launches on 16-wave workgroups, one per CU (MIPGPU_WIDE: 0 = never, 1 = every small
-// launch; default: below kWideItemsPerGroup items per CU at one slice).  Two 8-wave workgroups
-// on a CU progress at very different rates when both run an item (the SIMD arbiter serves the
-// older waves first: 98 vs 170 us for the two items of a CU in a 1080p frame,
-// profiles/r04_item_timeline_1frame.csv), so a launch of ~2 items per CU ends with one
-// workgroup running alone; one wide workgroup per CU has all 16 waves on one item's tasks.
-constexpr int kWideItemsPerGroup = 8;
+// Pair mode (16-wave workgroups): queue positions p and n - 1 - p run together on one
+// workgroup, in the time of both items' tasks (order_cost of the 16-wave lists).
+double pair_makespan(const std::vector<double> &order_cost, int nframes, int groups) {
+  const size_t n = order_cost.size() * (size_t)nframes;
+  std::vector<double> fin(groups, 0.0);  // min-heap of finish times
+  for (size_t p = 0; p < (n + 1) / 2; p++) {
+    double c = order_cost[p / nframes];
+    if (n - 1 - p != p) c += order_cost[(n - 1 - p) / nframes];
+    std::pop_heap(fin.begin(), fin.end(), std::greater<double>());
+    fin.back() += c;
+    std::push_heap(fin.begin(), fin.end(), std::greater<double>());
+  }
+  return *std::max_element(fin.begin(), fin.end());
+}
+
+// Small launches in pair mode, one 16-wave workgroup per CU (MIPGPU_WIDE: 0 = never, 1 =
+// every small launch; default: below kWideItemsPerGroup items per CU at one slice).  Two
+// 8-wave workgroups on a CU progress at very different rates when both run an item (the SIMD
+// arbiter serves the older waves first: 98 vs 170 us for the two items of a CU in a 1080p
+// frame, profiles/r04_item_timeline_1frame.csv), so a launch of ~2 items per CU ends with one
+// workgroup running alone; a pair-mode workgroup has all 16 waves on two items' tasks
+// (mip_search.hip pair_loop).
+constexpr int kWideItemsPerGroup = 4;
 bool wide_launch(long long items1, int cus) {
   const char *e = getenv("MIPGPU_WIDE");
   if (e && *e == '0') return false;
@@ -640,7 +643,8 @@ const mip_engine::Work &pick_work(mip_engine *e, int nframes, int nrange, bool a
     double best = 0;
     for (size_t i = 0; i < e->work.size(); i++) {
       if (e->work[i].wide != wide) continue;
-      const double m = lpt_makespan(e->work[i].order_cost, nframes, g);
+      const double m = wide ? pair_makespan(e->work[i].order_cost, nframes, g)
+                            : lpt_makespan(e->work[i].order_cost, nframes, g);
       if (ch < 0 || m < best) ch = (int)i, best = m;
     }
   }
@@ -755,7 +759,6 @@ int mip_engine_destroy(mip_engine *e) {
     if (e->d_fixup[m]) (void)hipFree(e->d_fixup[m]);
   }
   if (e->d_queue) (void)hipFree(e->d_queue);
-  if (e->d_task_ctr) (void)hipFree(e->d_task_ctr);
   if (e->h_status) (void)hipHostFree(e->h_status);
   for (hipEvent_t ev : e->queue_done)
     if (ev) (void)hipEventDestroy(ev);
@@ -857,10 +860,6 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0, false)) < 1 ||
         (e->resident_wide[alt] = mipgpu::search_resident_groups(alt != 0, true)) < 1)
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
-  e->help_cap = (uint32_t)kSmallLaunchItemsPerGroup * (uint32_t)std::max(e->resident[0], e->resident[1]);
-  ALLOC(e->d_task_ctr, (size_t)e->help_cap * mip_engine::kQueueSlots * sizeof(uint32_t));
-  if (hipMemset(e->d_task_ctr, 0, (size_t)e->help_cap * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
-    return cleanup(fail("hipMemset failed"));
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
   const CtuVariants cv = ctu_variants(width, height, o.filter);
   if (cv.pattern.size() > (size_t)mipgpu::kMaxCtuVariants)
@@ -1066,8 +1065,6 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const int slot = e->queue.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + mipgpu::kQueueWords * slot;
-  a.task_ctr = help_enabled() ? e->d_task_ctr + (size_t)e->help_cap * slot : nullptr;  // launch_search keeps
-  a.help_cap = e->help_cap;                                                            // it for small launches
   const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, s);
   if (le != hipSuccess) {
     e->queue.failed(slot);  // the pair is cleared before its next use
