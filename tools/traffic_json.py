@@ -14,7 +14,7 @@ import sys
 root, key, out = sys.argv[1], sys.argv[2], sys.argv[3]
 COUNTERS = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
             "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_ACTIVE_INST_VALU2")
-SEARCH = "mip_search_kernel<false, false, true>"         # original-reference search (the bench `value`)
+SEARCH = "mip_search_kernel<false, false, true, 8>"      # original-reference search (the bench `value`)
 FILTER = "filter_kernel<2, true, false>"    # BASELINE configs[2] filter (bench `filter`)
 
 

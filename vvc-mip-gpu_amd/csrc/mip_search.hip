@@ -1430,14 +1430,10 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
 // taken after the current one instead; launches with fewer than MIP_PREFETCH_MIN_ITEMS items
 // per workgroup do not prefetch at all (1-frame launches measured -9 % with the prefetching
 // kernel).  The ALT lattice leaves no LDS for a second window.
-// Pair mode (NW = kWideWaves): two items' windows (and ALT lattices) at once.
-template <bool ALT, bool PF, int NW>
-constexpr int kOrgTiles = (PF && !ALT) || NW == kWideWaves ? 2 : 1;
-template <bool ALT, int NW>
-constexpr int kLatTiles = ALT ? (NW == kWideWaves ? 2 : 1) : 0;
+template <bool ALT, bool PF>
+constexpr int kOrgTiles = PF && !ALT ? 2 : 1;
 constexpr int kCounterWords = 12;  // [parity]: next task, finished waves, item, item taken late;
                                    // [8]: chunks this workgroup has found empty (take_item)
-                                   // (pair mode: [0] next task, [1], [2] the pair's items)
 
 // The launch's items in kQueueChunks contiguous chunks (fewer if the grid is smaller), chunk
 // c = [chunk_begin(c), chunk_begin(c + 1)) with its own counter a.queue[c].  Workgroup b
@@ -1475,36 +1471,6 @@ __device__ __forceinline__ bool far_from_end(const SearchArgs &a, uint32_t item)
   return item >= b && item + 3 * (gridDim.x / k) < e;
 }
 constexpr uint32_t kTakeItem = 0xffffffffu;  // "take the next item after this one" (PF)
-
-// Two items' windows staged at once (pair mode): every thread's loads of both windows are in
-// flight before its first LDS store.  b = false: the second item is absent.
-template <int NT>
-__device__ __forceinline__ void stage_tiles2(uint16_t *dst0, const uint16_t *frame0, int x0, int y0, uint16_t *dst1,
-                                             const uint16_t *frame1, int x1, int y1, bool b, int width, int height,
-                                             uint32_t *status) {
-  const WindowStager<NT> s0(frame0, width, height, x0, y0, (int)threadIdx.x);
-  const WindowStager<NT> s1(frame1, width, height, x1, y1, (int)threadIdx.x);
-  constexpr int N = WindowStager<NT>::N;
-  uint2 v0[N], v1[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    if (s0.valid(k)) v0[k] = s0.load(k);
-    if (b && s1.valid(k)) v1[k] = s1.load(k);
-  }
-  uint32_t bits = 0;
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    if (s0.valid(k)) {
-      bits |= v0[k].x | v0[k].y;
-      s0.store(dst0, k, v0[k]);
-    }
-    if (b && s1.valid(k)) {
-      bits |= v1[k].x | v1[k].y;
-      s1.store(dst1, k, v1[k]);
-    }
-  }
-  flag_above_10_bits(bits, status, kStatusOrig);
-}
 
 // CUs whose cost the reference leaves undefined (edge CTUs) of one item: MIP_COST_UNAVAILABLE,
 // no search (the whole workgroup).
@@ -1572,92 +1538,15 @@ __device__ __forceinline__ void stamp_item_start(uint64_t *clk) {
                          (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
 }
 
-// Pair mode (16-wave workgroups, one per CU; small launches, launch_search): a workgroup
-// takes two items at once -- queue positions p and nitems - 1 - p, i.e. with the longest-first
-// order (SearchArgs::order) a long item with a short one -- stages both windows and lets its
-// 16 waves take the two items' tasks from one LDS counter (interleaved, so both lists' long
-// tasks come first).  With two 8-wave workgroups per CU the SIMD arbiter serves the older
-// workgroup's waves first, and in a launch of ~2 items per CU the younger one finishes alone
-// at half the CU's issue rate (profiles/r04_item_timeline_1frame.csv); here no wave idles
-// until both items' last tasks are taken.
-template <bool ALT, bool DEC>
-__device__ __forceinline__ void pair_loop(const SearchArgs &a, uint16_t *org_buf, uint16_t *lattice, const uint8_t *w,
-                                          const uint8_t *zero, uint8_t *waves, uint32_t *counters, int wave, int lane) {
-  const uint32_t npairs = (a.nitems + 1) / 2;
-  for (;;) {
-    if (threadIdx.x == 0) {
-      const uint32_t p = atomicAdd(a.queue, 1u);  // one queue chunk (launch_search)
-      counters[1] = p < npairs ? p : a.nitems;
-      counters[2] = p < npairs && a.nitems - 1 - p != p ? a.nitems - 1 - p : a.nitems;
-      counters[0] = 0;
-    }
-    __syncthreads();
-    const uint32_t i0 = counters[1], i1 = counters[2];
-    if (i0 >= a.nitems) break;  // workgroup-uniform
-    const bool two = i1 < a.nitems;
-    const ItemPos p0(a, i0), p1(a, two ? i1 : i0);
-    const int vq0 = a.ctu_var[p0.ctu] * 4 + p0.quad, vq1 = a.ctu_var[p1.ctu] * 4 + p1.quad;
-    const int l0 = vq0 * a.slices + p0.slice, l1 = vq1 * a.slices + p1.slice;
-    const int tb0 = a.list_begin[l0], n0 = a.list_begin[l0 + 1] - tb0;
-    const int tb1 = a.list_begin[l1], n1 = two ? a.list_begin[l1 + 1] - tb1 : 0;
-    fill_unavailable<DEC>(a, p0.frame, p0.ctu, vq0, p0.slice);
-    if (two) fill_unavailable<DEC>(a, p1.frame, p1.ctu, vq1, p1.slice);
-    uint16_t *org0 = org_buf, *org1 = org_buf + kTileElems;
-    uint16_t *ref0 = ALT ? lattice : org0, *ref1 = ALT ? lattice + kLatElems : org1;
-    const size_t fofs0 = (size_t)p0.frame * a.width * a.height, fofs1 = (size_t)p1.frame * a.width * a.height;
-    if (n0 + n1 > 0) {  // workgroup-uniform
-      stage_tiles2<64 * kWideWaves>(org0, a.orig + fofs0, p0.fx0, p0.fy0, org1, a.orig + fofs1, p1.fx0, p1.fy0,
-                                    two && n1 > 0, a.width, a.height, a.status);
-      if (ALT) {
-        stage_lattice<64 * kWideWaves>(ref0, a.refs + fofs0, a.width, a.height, p0.fx0, p0.fy0, a.check_refs != 0, a.status);
-        if (two && n1 > 0)
-          stage_lattice<64 * kWideWaves>(ref1, a.refs + fofs1, a.width, a.height, p1.fx0, p1.fy0, a.check_refs != 0, a.status);
-      }
-      __syncthreads();
-      uint64_t *clk0 = a.wave_clock ? a.wave_clock + (size_t)i0 * kClockSlots : nullptr;
-      uint64_t *clk1 = a.wave_clock && two ? a.wave_clock + (size_t)i1 * kClockSlots : nullptr;
-      if (clk0 && threadIdx.x == 0) {
-        stamp_item_start(clk0);
-        if (clk1) stamp_item_start(clk1);
-      }
-      const int m = n0 < n1 ? n0 : n1;
-      for (;;) {
-        uint32_t tn = 0;
-        if (lane == 0) tn = atomicAdd(counters, 1u);
-        const int t = (int)__builtin_amdgcn_readfirstlane(tn);
-        if (t >= n0 + n1) break;
-        // tasks 0 .. 2m-1 alternate between the items (each list is longest first), then the
-        // rest of the longer list
-        const bool second = t < 2 * m ? (t & 1) != 0 : n1 > n0;
-        const int k = t < 2 * m ? t >> 1 : t - m;
-        const uint64_t c0 = clk0 ? __builtin_readcyclecounter() : 0;
-        const WaveTask task = a.tasks[(second ? tb1 : tb0) + k];
-        const Ctx x{&a, second ? org1 : org0, second ? ref1 : ref0, w, zero, waves + wave * kWaveBytes,
-                    second ? p1.ctu : p0.ctu, second ? p1.frame : p0.frame, second ? p1.fx0 : p0.fx0,
-                    second ? p1.fy0 : p0.fy0};
-        const RefTile<ALT> rt{x.ref};
-        dispatch_task<ALT, DEC>(x, rt, task, lane);
-        uint64_t *clk = second ? clk1 : clk0;
-        if (clk && lane == 0) {
-          if (k < kClockSlots - 3) clk[k] = __builtin_readcyclecounter() - c0;
-          atomicMax(reinterpret_cast<unsigned long long *>(clk + kClockSlots - 2),
-                    (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        }
-      }
-    }
-    __syncthreads();  // every wave is done with the windows and the counters
-  }
-}
-
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
-// NW: waves per workgroup (kSearchWaves; kWideWaves: pair mode, small launches)
+// NW: waves per workgroup (kSearchWaves; kWideWaves: one workgroup per CU, small launches)
 template <bool ALT, bool DEC, bool PF_, int NW>
 __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = PF_ && !ALT && NW == kSearchWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles windows
-  uint16_t *lattice = org_buf + kOrgTiles<ALT, PF, NW> * kTileElems;
-  uint8_t *w = smem + (kOrgTiles<ALT, PF, NW> * kTileElems + kLatTiles<ALT, NW> * kLatElems) * 2;
+  uint16_t *lattice = org_buf + kOrgTiles<ALT, PF> * kTileElems;
+  uint8_t *w = smem + (kOrgTiles<ALT, PF> * kTileElems + (ALT ? kLatElems : 0)) * 2;
   uint8_t *zero = w + kTableBytes;
   uint8_t *waves = zero + kZeroBytes;
   uint32_t *counters = reinterpret_cast<uint32_t *>(waves + NW * kWaveBytes);
@@ -1668,9 +1557,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
     reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 
-  if constexpr (NW == kWideWaves) {
-    pair_loop<ALT, DEC>(a, org_buf, lattice, w, zero, waves, counters, wave, lane);
-  } else {
   // Persistent workgroups (as many as are resident) take items = (frame, CTU, quadrant,
   // slice) from a device-wide queue (take_item), in order: the hardware's static round-robin of
   // workgroups over XCDs and CUs cannot balance items of unequal cost (edge CTUs).
@@ -1798,7 +1684,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
     }
     if (PF) par ^= 1;  // (a loop-carried parity costs the ALT kernel ~30 VGPRs)
   }
-  }
   // The last workgroup to leave resets the queue's counters for the next launch that uses it
   // (the host never runs two launches on one pair at the same time).
   if (threadIdx.x == 0) {
@@ -1880,9 +1765,8 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
 }  // namespace
 
 size_t search_lds_bytes(bool alt, bool pf, int waves) {
-  const bool wide = waves == kWideWaves;  // pair mode: two windows / lattices
-  return (size_t)(((pf && !alt) || wide ? 2 : 1) * kTileElems + (alt ? (wide ? 2 : 1) * kLatElems : 0)) * 2 +
-         kTableBytes + kZeroBytes + (size_t)waves * kWaveBytes + kCounterWords * 4;
+  return (size_t)((pf && !alt ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
+         (size_t)waves * kWaveBytes + kCounterWords * 4;
 }
 
 template <bool ALT, bool DEC, bool PF, int NW>
@@ -1929,7 +1813,6 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;
   if (dec && (!a.best_cost || !a.dfill_begin)) return hipErrorInvalidValue;
-  if (wide) a.chunks = 1;  // pair mode takes pairs from queue[0]
   const bool pf = !alt_refs && !wide && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
   const size_t lds = search_lds_bytes(alt_refs, pf, wide ? kWideWaves : kSearchWaves);
   const dim3 grid(groups);

@@ -588,28 +588,15 @@ double lpt_makespan(const std::vector<double> &order_cost, int nframes, int grou
   return *std::max_element(fin.begin(), fin.end());
 }
 
-// Pair mode (16-wave workgroups): queue positions p and n - 1 - p run together on one
-// workgroup, in the time of both items' tasks (order_cost of the 16-wave lists).
-double pair_makespan(const std::vector<double> &order_cost, int nframes, int groups) {
-  const size_t n = order_cost.size() * (size_t)nframes;
-  std::vector<double> fin(groups, 0.0);  // min-heap of finish times
-  for (size_t p = 0; p < (n + 1) / 2; p++) {
-    double c = order_cost[p / nframes];
-    if (n - 1 - p != p) c += order_cost[(n - 1 - p) / nframes];
-    std::pop_heap(fin.begin(), fin.end(), std::greater<double>());
-    fin.back() += c;
-    std::push_heap(fin.begin(), fin.end(), std::greater<double>());
-  }
-  return *std::max_element(fin.begin(), fin.end());
-}
-
-// Small launches in pair mode, one 16-wave workgroup per CU (MIPGPU_WIDE: 0 = never, 1 =
-// every small launch; default: below kWideItemsPerGroup items per CU at one slice).  Two
-// 8-wave workgroups on a CU progress at very different rates when both run an item (the SIMD
-// arbiter serves the older waves first: 98 vs 170 us for the two items of a CU in a 1080p
-// frame, profiles/r04_item_timeline_1frame.csv), so a launch of ~2 items per CU ends with one
-// workgroup running alone; a pair-mode workgroup has all 16 waves on two items' tasks
-// (mip_search.hip pair_loop).
+// Small launches on 16-wave workgroups, one per CU (MIPGPU_WIDE: 0 = never, 1 = every small
+// launch; default: below kWideItemsPerGroup items per CU at one slice).  Two 8-wave workgroups
+// on a CU progress at very different rates when both run an item (the SIMD arbiter serves the
+// older waves first: 98 vs 170 us for the two items of a CU in a 1080p frame,
+// profiles/r04_item_timeline_1frame.csv), so a launch of ~2 items per CU ends with one
+// workgroup running alone; a 16-wave workgroup has all its waves on one item's tasks.
+// Measured (profiles/r04_small_batch_wide.jsonl): 1 frame 0.185 -> 0.175 ms, 2 frames
+// 0.293 -> 0.314 ms (without a second workgroup the item tails and window stagings idle the
+// CU), 8-16 frames -9 %.
 constexpr int kWideItemsPerGroup = 4;
 bool wide_launch(long long items1, int cus) {
   const char *e = getenv("MIPGPU_WIDE");
@@ -643,8 +630,7 @@ const mip_engine::Work &pick_work(mip_engine *e, int nframes, int nrange, bool a
     double best = 0;
     for (size_t i = 0; i < e->work.size(); i++) {
       if (e->work[i].wide != wide) continue;
-      const double m = wide ? pair_makespan(e->work[i].order_cost, nframes, g)
-                            : lpt_makespan(e->work[i].order_cost, nframes, g);
+      const double m = lpt_makespan(e->work[i].order_cost, nframes, g);
       if (ch < 0 || m < best) ch = (int)i, best = m;
     }
   }
