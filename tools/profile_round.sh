@@ -20,6 +20,24 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$RAW/trace" -o run --outp
   python3 bench.py --steps 10 $ARGS > "$OUT/trace_bench.json" 2> "$RAW/trace.err" || { tail -20 "$RAW/trace.err"; exit 1; }
 find "$RAW/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 python3 -c "import sys; sys.path.insert(0, 'vvc-mip-gpu_amd'); import mipgpu; print(mipgpu.build_id())" > "$OUT/build_id.txt"
+# the dominant kernel over the bench's timed steps only (kernel_stats.csv averages the warmup
+# launches in too), next to the bench line of the same profiled command
+python3 - "$RAW/trace" "$OUT" <<'PY' || echo "(timed-launch average unavailable)"
+import csv, glob, json, sys
+raw, out = sys.argv[1], sys.argv[2]
+line = json.loads(open(out + "/trace_bench.json").read().strip().splitlines()[-1])
+rows = [r for f in glob.glob(raw + "/**/*kernel_trace.csv", recursive=True) for r in csv.DictReader(open(f))
+        if "mip_search_kernel<false, false, true, 8>" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+timed = rows[-line["steps"]:]
+dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
+rec = {"kernel": "mip_search_kernel<false, false, true, 8>", "build_id": line["build_id"], "launches": len(rows),
+       "timed_launches": len(dur), "timed_avg_ms": round(sum(dur) / len(dur), 4), "timed_min_ms": round(min(dur), 4),
+       "timed_max_ms": round(max(dur), 4), "bench_ms_per_step_same_run": line["ms_per_step"],
+       "bench_kernel_ms_same_run": line["roofline"]["kernel_ms_per_launch"]}
+json.dump(rec, open(out + "/kernel_timed.json", "w"), indent=1)
+print(json.dumps(rec))
+PY
 head -5 "$OUT/kernel_stats.csv"
 i=0
 while read -r counters; do
