@@ -1542,7 +1542,7 @@ __device__ __forceinline__ void stamp_item_start(uint64_t *clk) {
 // NW: waves per workgroup (kSearchWaves; kWideWaves: one workgroup per CU, small launches)
 template <bool ALT, bool DEC, bool PF_, int NW>
 __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
-  constexpr bool PF = PF_ && !ALT;
+  constexpr bool PF = PF_ && !ALT && NW == kSearchWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles windows
   uint16_t *lattice = org_buf + kOrgTiles<ALT, PF> * kTileElems;
@@ -1642,9 +1642,7 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
         // (far_from_end: in the workgroup's own chunk, more than three rounds of its
         // workgroups left)
         uint32_t n = kTakeItem;
-        // (16-wave workgroups run small launches of ~2 items each: the next item is always
-        // taken early -- one item per workgroup is left after the first round)
-        if (lane == 0 && (NW == kWideWaves || far_from_end(a, item))) n = take_item(a, counters + 8);
+        if (lane == 0 && far_from_end(a, item)) n = take_item(a, counters + 8);
         const uint32_t nitem = __builtin_amdgcn_readfirstlane(n);
         if (nitem < a.nitems) {  // (kTakeItem >= nitems)
           const ItemPos np(a, nitem);
@@ -1787,8 +1785,7 @@ int search_resident_groups(bool alt, bool wide) {
   int per_cu;
   if (wide)
     per_cu = alt ? std::min(resident_per_cu<true, false, false, L>(), resident_per_cu<true, true, false, L>())
-                 : std::min({resident_per_cu<false, false, false, L>(), resident_per_cu<false, true, false, L>(),
-                             resident_per_cu<false, false, true, L>(), resident_per_cu<false, true, true, L>()});
+                 : std::min(resident_per_cu<false, false, false, L>(), resident_per_cu<false, true, false, L>());
   else
     per_cu = alt ? std::min(resident_per_cu<true, false, false, S>(), resident_per_cu<true, true, false, S>())
                  : std::min({resident_per_cu<false, false, false, S>(), resident_per_cu<false, true, false, S>(),
@@ -1816,9 +1813,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;
   if (dec && (!a.best_cost || !a.dfill_begin)) return hipErrorInvalidValue;
-  const char *wpf = getenv("MIPGPU_WIDE_PF");  // A/B knob: 0 = 16-wave launches without prefetch
-  const bool pf = !alt_refs && (wide ? !(wpf && *wpf == '0')
-                                     : a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups);
+  const bool pf = !alt_refs && !wide && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
   const size_t lds = search_lds_bytes(alt_refs, pf, wide ? kWideWaves : kSearchWaves);
   const dim3 grid(groups);
   constexpr int S = kSearchWaves, L = kWideWaves;
@@ -1827,9 +1822,6 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
     if (alt_refs) {
       if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true, false, L>), grid, block, lds, s, a);
       else hipLaunchKernelGGL((mip_search_kernel<true, false, false, L>), grid, block, lds, s, a);
-    } else if (pf) {
-      if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, true, L>), grid, block, lds, s, a);
-      else hipLaunchKernelGGL((mip_search_kernel<false, false, true, L>), grid, block, lds, s, a);
     } else {
       if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, false, L>), grid, block, lds, s, a);
       else hipLaunchKernelGGL((mip_search_kernel<false, false, false, L>), grid, block, lds, s, a);
