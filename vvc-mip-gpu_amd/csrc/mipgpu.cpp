@@ -599,6 +599,7 @@ double lpt_makespan(const std::vector<double> &order_cost, int nframes, int grou
 // CU), 8-16 frames -9 %.
 constexpr int kWideItemsPerGroup = 4;
 bool wide_launch(long long items1, int cus) {
+  if (cus < 1) return false;  // no 16-wave workgroup fits a CU of this device
   const char *e = getenv("MIPGPU_WIDE");
   if (e && *e == '0') return false;
   if (e && *e == '1') return true;
@@ -842,10 +843,12 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     return cleanup(fail("hipHostGetDevicePointer (status words) failed"));
   if (hipEventCreateWithFlags(&e->refs_done, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail("hipEventCreate failed"));
-  for (int alt = 0; alt < 2; alt++)
-    if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0, false)) < 1 ||
-        (e->resident_wide[alt] = mipgpu::search_resident_groups(alt != 0, true)) < 1)
+  for (int alt = 0; alt < 2; alt++) {
+    if ((e->resident[alt] = mipgpu::search_resident_groups(alt != 0, false)) < 1)
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
+    // 16-wave workgroups (small launches) are optional: 0 when one does not fit a CU
+    e->resident_wide[alt] = mipgpu::search_resident_groups(alt != 0, true);
+  }
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
   const CtuVariants cv = ctu_variants(width, height, o.filter);
   if (cv.pattern.size() > (size_t)mipgpu::kMaxCtuVariants)
