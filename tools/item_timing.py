@@ -32,7 +32,7 @@ n = raw.size // SLOTS
 raw = raw.reshape(n, SLOTS)
 t0, t1, hw = raw[:, SLOTS - 3].astype(np.int64), raw[:, SLOTS - 2].astype(np.int64), raw[:, SLOTS - 1]
 clk = raw[:, :SLOTS - 3].astype(np.int64)
-per_item = clk.sum(axis=1) / 8.0  # 8 waves share an item's tasks
+per_item = clk.sum(axis=1)  # cycles of all the item's tasks (shader clock; 8 or 16 waves share them)
 # placement: HW_ID cu_id bits 11:8, sh 12, se 15:13; XCC_ID low 4 bits of the high word
 ne = per_item > 0
 s0 = raw[:, SLOTS - 3].astype(np.int64)
@@ -41,7 +41,7 @@ cu = ((hw >> 8) & 15) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 7) << 5) | (((h
 rows = np.stack([np.arange(n)[ne], (s0[ne] - t0), (t1[ne] - t0), cu[ne].astype(np.int64), per_item[ne].astype(np.int64)], 1)
 out = os.environ.get("ITEM_CSV")
 if out:
-    np.savetxt(out, rows, fmt="%d", delimiter=",", header="item,start_10ns,end_10ns,cu,task_cycles_per_wave")
+    np.savetxt(out, rows, fmt="%d", delimiter=",", header="item,start_10ns,end_10ns,cu,task_cycles_sum")
 dur = (rows[:, 2] - rows[:, 1]) / 100.0
 print(json.dumps({"launch_span_us": float(rows[:, 2].max() / 100.0), "last_start_us": float(rows[:, 1].max() / 100.0),
                   "item_us_p10_p50_p90_max": [round(float(np.percentile(dur, p)), 1) for p in (10, 50, 90, 100)],
