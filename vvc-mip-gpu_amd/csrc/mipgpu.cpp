@@ -339,13 +339,6 @@ CtuVariants ctu_variants(int width, int height, int filter) {
   return v;
 }
 
-// Tail refinement levels of a task list (build_work): 16-wave lists only by default.
-int tail_split_levels(int waves) {
-  const char *e = getenv("MIPGPU_TAIL_SPLIT");  // A/B knob: levels for the 16-wave lists
-  if (waves != mipgpu::kWideWaves) return 0;
-  return e && atoi(e) >= 0 ? std::min(atoi(e), 4) : 1;
-}
-
 double pair_cost(int cls, int ncu) {
   const int w = mipgpu::kClassW[cls], h = mipgpu::kClassH[cls];
   const int sid = mipgpu::class_size_id(w, h), v = mipgpu::kClassV[cls];
@@ -446,41 +439,6 @@ WorkLists build_work(int slices, int waves, int width, int height, const CtuVari
       }
     }
     std::stable_sort(cut.begin(), cut.end(), [](const Piece &a, const Piece &b) { return a.cost > b.cost; });
-    // Tail refinement (16-wave lists: small launches, where no second workgroup fills the
-    // CU while an item's last tasks run): the pieces that make up the last round of the list
-    // (about one cap-sized piece per wave) are halved, and that again for the last half
-    // round, so the waves of an item finish closer together; the extra task prologues are
-    // paid only there.  (MIPGPU_TAIL_SPLIT = levels; default tail_split_levels.)
-    for (int level = 0; level < tail_split_levels(waves); level++) {
-      const double tail = waves * cap / (double)(1 << level);
-      double acc = 0;
-      size_t first = cut.size();
-      while (first > 0 && acc < tail) acc += cut[--first].cost;
-      std::vector<Piece> head(cut.begin(), cut.begin() + first), rest;
-      for (size_t i = first; i < cut.size(); i++) {
-        const Piece &p = cut[i];
-        const int np = p.t.q1 - p.t.q0;
-        if (np < 2) {
-          rest.push_back(p);
-          continue;
-        }
-        // a CU whose pairs were all in one task is now split over two (decisions only: its
-        // argmin meets in a packed atomicMin entry, initialised by dec_split_kernel)
-        const int sid = mipgpu::class_size_id(mipgpu::kClassW[p.t.cls], mipgpu::kClassH[p.t.cls]);
-        if (p.t.q0 == 0 && p.t.q1 == (sid == 2 ? 6 : (sid == 1 ? 8 : 16)))
-          for (uint32_t j = 0; j < p.t.ncu; j++) wl.split.push_back(wl.jobs[p.t.cu0 + j].cu);
-        for (int h = 0; h < 2; h++) {
-          Piece c = p;
-          c.t.q0 = (uint8_t)(p.t.q0 + np * h / 2);
-          c.t.q1 = (uint8_t)(p.t.q0 + np * (h + 1) / 2);
-          c.cost = (p.cost - 150.0) * (c.t.q1 - c.t.q0) / np + 150.0;
-          rest.push_back(c);
-        }
-      }
-      std::stable_sort(rest.begin(), rest.end(), [](const Piece &a, const Piece &b) { return a.cost > b.cost; });
-      head.insert(head.end(), rest.begin(), rest.end());
-      cut.swap(head);
-    }
     const int bins = slices;
     std::vector<double> load(bins, 0.0);
     std::vector<std::vector<mipgpu::WaveTask>> lists(bins);
