@@ -120,3 +120,18 @@ def test_pmc_profile_of_another_build_is_not_used(tmp_path, monkeypatch):
     assert rec == {} and "src:aaaa" in why
     rec, why = bench.load_pmc(64, 64, 3, "src:aaaa git:x")
     assert rec == {}
+
+
+def test_valu_section_reports_both_issue_peaks():
+    """The `valu` object prices the measured VALU rate against the single-issue rate (`frac`)
+    and the two-per-quad-cycle dual-issue peak (`frac_of_dual_peak`)."""
+    pmc = {"valu_insts_per_launch": 30.0e9, "valu_issue_utilization": 0.98,
+           "valu_insts_per_simd_quad_cycle": 0.98, "valu_dual_issue_share": 0.054}
+    v = bench.valu_section(pmc, 50.0, 99.6e6 * 510 * 384)
+    rate = 30.0e9 / 0.050
+    assert v["frac"] == round(rate / bench.VALU_PEAK_INSTS, 4)
+    assert v["frac_of_dual_peak"] == round(rate / (2 * bench.VALU_PEAK_INSTS), 4)
+    assert v["dual_peak"] == round(2 * bench.VALU_PEAK_INSTS / 1e9, 1)
+    # without a PMC profile of this build the measured fields stay null
+    v0 = bench.valu_section({}, 50.0, 1.0)
+    assert v0["frac"] is None and "frac_of_dual_peak" not in v0
