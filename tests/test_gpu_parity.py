@@ -633,33 +633,27 @@ def test_tickets_dropped_on_another_thread(gpu_available):
 @pytest.mark.parametrize("w,h,n,filt,k", [(1920, 1080, 1, None, 0), (416, 240, 3, "filterFrame_2d_int_quarterCtu", 1),
                                           (264, 136, 2, None, 0)])
 def test_small_launch_shapes_agree(gpu_available, monkeypatch, w, h, n, filt, k):
-    """Small launches run one 16-wave workgroup per CU
-    (MIPGPU_WIDE; mip_search_kernel<..., 16>), or the two 8-wave workgroups of a CU on a
-    shared pair of items (MIPGPU_POOL, original references; pool_loop), or 8-wave workgroups
-    on their own items, with the items longest first or in raster order (MIPGPU_ORDER).  The
-    knobs are read per launch (mipgpu.cpp wide_launch, pool_launch, lpt_order_enabled): one
-    engine runs every combination, and every combination must give the same cost / SAD / SATD
-    tables and decisions (full table and fused decisions-only), equal to the oracle's."""
+    """Small launches run one 16-wave workgroup per CU below 4 items
+    per CU (MIPGPU_WIDE; mip_search_kernel<..., 16>) and 8-wave workgroups above, with the
+    items longest first (MIPGPU_ORDER).  Both knobs are read per launch (mipgpu.cpp
+    wide_launch, lpt_order_enabled): one engine runs every combination, and every
+    combination must give the same cost / SAD / SATD tables and decisions (full table and
+    fused decisions-only), equal to the oracle's."""
     frames = synth_frames(w, h, n, 0x5A11 + w, 1)
     outs = []
     with MipEngine(w, h, max_batch=n, filter=filt, kernel_idx=k, want_sad_satd=True) as eng:
-        for wide, pool, order in (("1", "0", "1"), ("0", "1", "1"), ("0", "0", "1"), ("1", "0", "0"),
-                                  ("0", "1", "0"), ("0", "0", "0")):
+        for wide, order in (("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")):
             monkeypatch.setenv("MIPGPU_WIDE", wide)
-            monkeypatch.setenv("MIPGPU_POOL", pool)
             monkeypatch.setenv("MIPGPU_ORDER", order)
             full = eng.search(frames, best=True, sad_satd=True)
             dec = eng.search(frames, costs=False, best=True)
-            # twice in a row: the pool words and counters are left zero for the next launch
-            again = eng.search(frames, best=True)
-            outs.append(((wide, pool, order), full, dec, again))
-    ref = outs[0][1]
-    for knobs, full, dec, again in outs:
+            outs.append((wide, order, full, dec))
+    ref = outs[0][2]
+    for wide, order, full, dec in outs:
         for key in ("cost", "sad", "satd", "best_mode", "best_cost"):
-            assert np.array_equal(full[key], ref[key]), (knobs, key)
+            assert np.array_equal(full[key], ref[key]), (wide, order, key)
         for key in ("best_mode", "best_cost"):
-            assert np.array_equal(dec[key], ref[key]), (knobs, "dec", key)
-        assert np.array_equal(again["cost"], ref["cost"]), (knobs, "again")
+            assert np.array_equal(dec[key], ref[key]), (wide, order, "dec", key)
     cost, sad, satd = O.engine_search(frames[n - 1], filt, k, want_sad_satd=True)
     assert np.array_equal(ref["cost"][n - 1], cost)
     assert np.array_equal(ref["sad"][n - 1], sad) and np.array_equal(ref["satd"][n - 1], satd)

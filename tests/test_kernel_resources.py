@@ -31,9 +31,9 @@ def _named(kernels, part):
 
 
 def test_every_kernel_variant_present(kernels):
-    # {orig, alt} x {table, decisions} x prefetch (orig) with 8-wave workgroups, {orig, alt} x
-    # {table, decisions} with 16-wave ones, and the pool variants (orig x {table, decisions})
-    assert len(_named(kernels, "mip_search_kernel")) == 12
+    # {orig, alt} x {table, decisions} x prefetch (orig), and the 16-wave variants of small
+    # launches ({orig, alt} x {table, decisions}, no prefetch)
+    assert len(_named(kernels, "mip_search_kernel")) == 10
     assert len(_named(kernels, "filter_kernel")) == 8      # radius x int/float x 2-D/separable
     for part in ("fixup_kernel", "best_mode_kernel", "dec_split_kernel"):
         _named(kernels, part)

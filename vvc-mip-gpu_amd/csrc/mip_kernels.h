@@ -105,13 +105,7 @@ struct SearchArgs {
   // (read by the host after the search; only ever written when the contract is broken).
   uint32_t *status;
   int check_refs;
-  // Pool mode (small launches, mip_search.hip pool_loop): per-CU words
-  // [cu][kCuPoolWords] (arrivals, published pair) over the kCuPoolIndex values of the CU
-  // index, then one task counter per pair; zero at launch, left zero.  Null: not pool mode.
-  uint32_t *cu_pool;
 };
-constexpr int kCuPoolIndex = 4096, kCuPoolWords = 2, kPoolPairs = 4096;
-constexpr int kCuPoolTotalWords = kCuPoolIndex * kCuPoolWords + kPoolPairs;
 constexpr int kStatusOrig = 0, kStatusRefs = 1, kStatusWords = 4;
 constexpr uint32_t kAbove10Bits = 0xfc00fc00u;  // any of bits 10..15 in either half
 constexpr int kClockSlots = 128;
@@ -177,10 +171,7 @@ constexpr int kSearchWaves = 8, kWideWaves = 16;
 // Workgroups of the search kernel resident on the current device at once (persistent grid
 // size); computed once per engine (mip_engine_create), 0 on error.
 int search_resident_groups(bool alt_refs, bool wide);
-// pool: small launches in pool mode (original references, whole frames, a.cu_pool set, at most
-// kPoolPairs pairs of items)
-hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, bool wide, bool pool,
-                         hipStream_t s);
+hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s);
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 // Decisions only, CUs whose mode pairs are cut over several tasks (split CUs of the CTU's
 // variant: [split_begin[v], split_begin[v+1]) of `split`, at most max_split per variant):

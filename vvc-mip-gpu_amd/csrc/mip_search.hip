@@ -1538,107 +1538,9 @@ __device__ __forceinline__ void stamp_item_start(uint64_t *clk) {
                          (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
 }
 
-// CU index of the executing workgroup: HW_ID (CU 11:8, SH 12, SE 15:13) and XCC_ID (3:0);
-// unique per CU, < kCuPoolIndex.
-__device__ __forceinline__ uint32_t cu_index() {
-  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-  return ((hw >> 8) & 15) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 7) << 5) | ((xcc & 7) << 8);
-}
-
-// Pool mode (one-frame launches, original references; launch_search): the two workgroups of a
-// CU share one pair of items -- queue positions p and nitems - 1 - p, with the longest-first
-// order (SearchArgs::order) a long item and a short one -- and take the two items' tasks
-// from one counter in global memory, so neither finishes alone while the other starves (the
-// SIMD arbiter serves the older workgroup's waves first: 98 vs 170 us for the two items of a
-// CU when each runs its own, profiles/r04_item_timeline_1frame.csv).  The CU's workgroups
-// meet through its arrival counter: the first of each two takes a pair from the queue and
-// publishes it with the round's tag; the second waits for a tag at least its own (a later
-// round's pair is as good: every pair is run to its end by the workgroup that took it).
-// Each workgroup stages both windows; the first also writes the fills.
-template <bool DEC>
-__device__ __forceinline__ void pool_loop(const SearchArgs &a, uint16_t *org_buf, const uint8_t *w, const uint8_t *zero,
-                                          uint8_t *waves, uint32_t *counters, int wave, int lane) {
-  const uint32_t npairs = (a.nitems + 1) / 2;
-  uint32_t *slot = a.cu_pool + cu_index() * kCuPoolWords;
-  for (;;) {  // rounds: one pair per round for the CU's workgroups
-    if (threadIdx.x == 0) {
-      const uint32_t arr = atomicAdd(slot, 1u), tag = (arr >> 1) + 1;
-      uint32_t p;
-      if ((arr & 1) == 0) {
-        p = min(atomicAdd(a.queue, 1u), 0xffffu);
-        __hip_atomic_store(slot + 1, tag << 16 | p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        uint32_t v;
-        while (((v = __hip_atomic_load(slot + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 16) < tag)
-          __builtin_amdgcn_s_sleep(2);
-        p = v & 0xffffu;
-      }
-      counters[0] = (arr & 1) == 0;
-      counters[1] = p;
-    }
-    __syncthreads();
-    const uint32_t p = counters[1];
-    if (p >= npairs) return;  // workgroup-uniform
-    const uint32_t i0 = p, i1 = a.nitems - 1 - p;
-    const bool two = i1 != i0;
-    const ItemPos p0(a, i0), p1(a, i1);
-    const int vq0 = a.ctu_var[p0.ctu] * 4 + p0.quad, vq1 = a.ctu_var[p1.ctu] * 4 + p1.quad;
-    const int l0 = vq0 * a.slices + p0.slice, l1 = vq1 * a.slices + p1.slice;
-    const int tb0 = a.list_begin[l0], n0 = a.list_begin[l0 + 1] - tb0;
-    const int tb1 = a.list_begin[l1], n1 = two ? a.list_begin[l1 + 1] - tb1 : 0;
-    if (counters[0]) {
-      fill_unavailable<DEC>(a, p0.frame, p0.ctu, vq0, p0.slice);
-      if (two) fill_unavailable<DEC>(a, p1.frame, p1.ctu, vq1, p1.slice);
-    }
-    uint16_t *org0 = org_buf, *org1 = org_buf + kTileElems;
-    if (n0 + n1 > 0) {  // workgroup-uniform
-      if (n0 > 0)
-        stage_tile<64 * kSearchWaves>(org0, a.orig + (size_t)p0.frame * a.width * a.height, a.width, a.height, p0.fx0,
-                                      p0.fy0, a.status);
-      if (n1 > 0)
-        stage_tile<64 * kSearchWaves>(org1, a.orig + (size_t)p1.frame * a.width * a.height, a.width, a.height, p1.fx0,
-                                      p1.fy0, a.status);
-      __syncthreads();
-      uint64_t *clk0 = a.wave_clock ? a.wave_clock + (size_t)i0 * kClockSlots : nullptr;
-      uint64_t *clk1 = a.wave_clock && two ? a.wave_clock + (size_t)i1 * kClockSlots : nullptr;
-      if (clk0 && threadIdx.x == 0 && counters[0]) {
-        stamp_item_start(clk0);
-        if (clk1) stamp_item_start(clk1);
-      }
-      uint32_t *ctr = a.cu_pool + kCuPoolIndex * kCuPoolWords + p;
-      const int m = n0 < n1 ? n0 : n1;
-      for (;;) {
-        uint32_t tn = 0;
-        if (lane == 0) tn = atomicAdd(ctr, 1u);
-        const int t = (int)__builtin_amdgcn_readfirstlane(tn);
-        if (t >= n0 + n1) break;
-        // tasks 0 .. 2m-1 alternate between the items (each list is longest first), then the
-        // rest of the longer list
-        const bool second = t < 2 * m ? (t & 1) != 0 : n1 > n0;
-        const int k = t < 2 * m ? t >> 1 : t - m;
-        const uint64_t c0 = clk0 ? __builtin_readcyclecounter() : 0;
-        const WaveTask task = a.tasks[(second ? tb1 : tb0) + k];
-        const Ctx x{&a, second ? org1 : org0, second ? org1 : org0, w, zero, waves + wave * kWaveBytes,
-                    second ? p1.ctu : p0.ctu, second ? p1.frame : p0.frame, second ? p1.fx0 : p0.fx0,
-                    second ? p1.fy0 : p0.fy0};
-        const RefTile<false> rt{x.ref};
-        dispatch_task<false, DEC>(x, rt, task, lane);
-        uint64_t *clk = second ? clk1 : clk0;
-        if (clk && lane == 0) {
-          if (k < kClockSlots - 3) clk[k] = __builtin_readcyclecounter() - c0;
-          atomicMax(reinterpret_cast<unsigned long long *>(clk + kClockSlots - 2),
-                    (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        }
-      }
-    }
-    __syncthreads();  // every wave is done with the windows and the round's counters
-  }
-}
-
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
 // NW: waves per workgroup (kSearchWaves; kWideWaves: one workgroup per CU, small launches)
-// POOL: pool mode (pool_loop; instantiated with the prefetching variant's two windows)
-template <bool ALT, bool DEC, bool PF_, int NW, bool POOL = false>
+template <bool ALT, bool DEC, bool PF_, int NW>
 __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = PF_ && !ALT && NW == kSearchWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1655,10 +1557,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
     reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 
-  if constexpr (POOL) {
-    static_assert(!ALT && PF && NW == kSearchWaves, "pool mode: original references, two windows, 8 waves");
-    pool_loop<DEC>(a, org_buf, w, zero, waves, counters, wave, lane);
-  } else {
   // Persistent workgroups (as many as are resident) take items = (frame, CTU, quadrant,
   // slice) from a device-wide queue (take_item), in order: the hardware's static round-robin of
   // workgroups over XCDs and CUs cannot balance items of unequal cost (edge CTUs).
@@ -1786,25 +1684,13 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
     }
     if (PF) par ^= 1;  // (a loop-carried parity costs the ALT kernel ~30 VGPRs)
   }
-  }
   // The last workgroup to leave resets the queue's counters for the next launch that uses it
-  // (the host never runs two launches on one pair at the same time); pool mode: the per-CU
-  // words and the pairs' task counters too.
-  if constexpr (POOL) __syncthreads();  // every wave is past the pair's task counter
+  // (the host never runs two launches on one pair at the same time).
   if (threadIdx.x == 0) {
     __threadfence();
-    const bool last = atomicAdd(a.queue + kQueueChunks, 1u) == gridDim.x - 1;
-    if (last) {
+    if (atomicAdd(a.queue + kQueueChunks, 1u) == gridDim.x - 1) {
       for (int c = 0; c < kQueueChunks; c++) atomicExch(a.queue + c, 0u);
       atomicExch(a.queue + kQueueChunks, 0u);
-    }
-    if (POOL) counters[10] = last;
-  }
-  if constexpr (POOL) {
-    __syncthreads();
-    if (counters[10]) {
-      const uint32_t nw = kCuPoolIndex * kCuPoolWords + (a.nitems + 1) / 2;
-      for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) atomicExch(a.cu_pool + i, 0u);
     }
   }
 }
@@ -1907,10 +1793,8 @@ int search_resident_groups(bool alt, bool wide) {
   return per_cu >= 1 ? cus * per_cu : 0;
 }
 
-hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, bool wide, bool pool,
-                         hipStream_t s) {
+hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s) {
   if (args.slices < 1 || !args.queue || !args.status || resident < 1) return hipErrorInvalidValue;
-  if (pool && (alt_refs || wide || !args.cu_pool)) return hipErrorInvalidValue;
   SearchArgs a = args;
   if (a.ctu0 < 0 || a.nrange < 1 || a.ctu0 + a.nrange > a.nctus) return hipErrorInvalidValue;
   const long long nitems = (long long)(4 * a.slices) * a.nrange * nframes;
@@ -1930,16 +1814,9 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const bool dec = a.cost == nullptr;
   if (dec && (!a.best_cost || !a.dfill_begin)) return hipErrorInvalidValue;
   const bool pf = !alt_refs && !wide && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
-  const size_t lds = search_lds_bytes(alt_refs, pf || pool, wide ? kWideWaves : kSearchWaves);
+  const size_t lds = search_lds_bytes(alt_refs, pf, wide ? kWideWaves : kSearchWaves);
   const dim3 grid(groups);
   constexpr int S = kSearchWaves, L = kWideWaves;
-  if (pool) {
-    // one queue counter (the pairs), a task counter per pair
-    if ((a.nitems + 1) / 2 > (uint32_t)kPoolPairs || a.chunks != 1) return hipErrorInvalidValue;  // (pair counters)
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, true, S, true>), grid, dim3(64 * S), lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<false, false, true, S, true>), grid, dim3(64 * S), lds, s, a);
-    return hipGetLastError();
-  }
   if (wide) {
     const dim3 block(64 * L);
     if (alt_refs) {

@@ -541,9 +541,6 @@ struct mip_engine {
   // launches on different streams never share one.
   static constexpr int kQueueSlots = 16;
   uint32_t *d_queue = nullptr;
-  // pool mode of small launches (SearchArgs::cu_pool): kCuPoolTotalWords per queue slot (a
-  // slot's words are used by the launch that holds the slot; the kernel leaves them zero)
-  uint32_t *d_cu_pool = nullptr;
   hipEvent_t queue_done[kQueueSlots] = {};
   struct QueueOps {
     mip_engine *e;
@@ -551,9 +548,7 @@ struct mip_engine {
     int record(int slot, hipStream_t s) const { return hipEventRecord(e->queue_done[slot], s) != hipSuccess; }
     int clear(int slot, hipStream_t s) const {
       return hipMemsetAsync(e->d_queue + mipgpu::kQueueWords * slot, 0, mipgpu::kQueueWords * sizeof(uint32_t), s) !=
-                 hipSuccess ||
-             hipMemsetAsync(e->d_cu_pool + (size_t)mipgpu::kCuPoolTotalWords * slot, 0,
-                            mipgpu::kCuPoolTotalWords * sizeof(uint32_t), s) != hipSuccess;
+             hipSuccess;
     }
     int sync(hipStream_t s) const { return hipStreamSynchronize(s) != hipSuccess; }
   };
@@ -609,21 +604,6 @@ bool wide_launch(long long items1, int cus) {
   if (e && *e == '0') return false;
   if (e && *e == '1') return true;
   return items1 < (long long)kWideItemsPerGroup * cus;
-}
-
-// Pool mode (MIPGPU_POOL: 0 = never, 1 = every small 8-wave whole-frame launch; default:
-// below kPoolItemsPerGroup items per workgroup at one slice): the two workgroups of a CU
-// share a pair of items' tasks (mip_search.hip pool_loop).
-constexpr int kPoolItemsPerGroup = 2;
-bool pool_launch(const mip_engine *e, const mip_engine::Work &w, bool alt, int nframes, int nrange) {
-  if (alt || w.wide || nrange != e->nctus) return false;
-  const long long items = 4LL * w.slices * nrange * nframes;
-  if ((items + 1) / 2 > mipgpu::kPoolPairs || items >= (long long)kSmallLaunchItemsPerGroup * e->resident[0])
-    return false;  // (one queue chunk: launch_search)
-  const char *v = getenv("MIPGPU_POOL");
-  if (v && *v == '0') return false;
-  if (v && *v == '1') return true;
-  return 4LL * nrange * nframes < (long long)kPoolItemsPerGroup * e->resident[0];
 }
 
 // Work lists for a launch of `nframes`: items (quadrant x slice) for the persistent grid.
@@ -766,7 +746,6 @@ int mip_engine_destroy(mip_engine *e) {
     if (e->d_fixup[m]) (void)hipFree(e->d_fixup[m]);
   }
   if (e->d_queue) (void)hipFree(e->d_queue);
-  if (e->d_cu_pool) (void)hipFree(e->d_cu_pool);
   if (e->h_status) (void)hipHostFree(e->h_status);
   for (hipEvent_t ev : e->queue_done)
     if (ev) (void)hipEventDestroy(ev);
@@ -851,10 +830,6 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     ALLOC(e->d_satd, ncost * 4);
   }
   ALLOC(e->d_best, ncu * o.best_k);
-  ALLOC(e->d_cu_pool, (size_t)mipgpu::kCuPoolTotalWords * mip_engine::kQueueSlots * sizeof(uint32_t));
-  if (hipMemset(e->d_cu_pool, 0, (size_t)mipgpu::kCuPoolTotalWords * mip_engine::kQueueSlots * sizeof(uint32_t)) !=
-      hipSuccess)
-    return cleanup(fail("hipMemset failed"));
   ALLOC(e->d_queue, mipgpu::kQueueWords * mip_engine::kQueueSlots * sizeof(uint32_t));
   if (hipMemset(e->d_queue, 0, mipgpu::kQueueWords * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail("hipMemset failed"));
@@ -1079,9 +1054,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const int slot = e->queue.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + mipgpu::kQueueWords * slot;
-  const bool pool = pool_launch(e, work, alt, nframes, nrange);
-  a.cu_pool = pool ? e->d_cu_pool + (size_t)mipgpu::kCuPoolTotalWords * slot : nullptr;
-  const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, pool, s);
+  const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, s);
   if (le != hipSuccess) {
     e->queue.failed(slot);  // the pair is cleared before its next use
     return fail("search launch failed: %s", hipGetErrorString(le));
