@@ -634,26 +634,30 @@ def test_tickets_dropped_on_another_thread(gpu_available):
                                           (264, 136, 2, None, 0)])
 def test_small_launch_shapes_agree(gpu_available, monkeypatch, w, h, n, filt, k):
     """Small launches run one 16-wave workgroup per CU below 4 items
-    per CU (MIPGPU_WIDE; mip_search_kernel<..., 16>) and 8-wave workgroups above, with the
-    items longest first (MIPGPU_ORDER).  Both knobs are read per launch (mipgpu.cpp
-    wide_launch, lpt_order_enabled): one engine runs every combination, and every
+    per CU (MIPGPU_WIDE; mip_search_kernel<..., 16>) -- with original references and the
+    longest-first order two items at a time (pair mode, MIPGPU_PAIR; the fill-only items
+    ride along) -- and 8-wave workgroups above, with the items longest first or in raster
+    order (MIPGPU_ORDER).  The knobs are read per launch (mipgpu.cpp wide_launch,
+    lpt_order_enabled, the pair knob): one engine runs every combination, and every
     combination must give the same cost / SAD / SATD tables and decisions (full table and
     fused decisions-only), equal to the oracle's."""
     frames = synth_frames(w, h, n, 0x5A11 + w, 1)
     outs = []
     with MipEngine(w, h, max_batch=n, filter=filt, kernel_idx=k, want_sad_satd=True) as eng:
-        for wide, order in (("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")):
+        for wide, pair, order in (("1", "1", "1"), ("1", "0", "1"), ("0", "1", "1"), ("1", "1", "0"),
+                                  ("0", "1", "0")):
             monkeypatch.setenv("MIPGPU_WIDE", wide)
+            monkeypatch.setenv("MIPGPU_PAIR", pair)
             monkeypatch.setenv("MIPGPU_ORDER", order)
             full = eng.search(frames, best=True, sad_satd=True)
             dec = eng.search(frames, costs=False, best=True)
-            outs.append((wide, order, full, dec))
-    ref = outs[0][2]
-    for wide, order, full, dec in outs:
+            outs.append(((wide, pair, order), full, dec))
+    ref = outs[0][1]
+    for knobs, full, dec in outs:
         for key in ("cost", "sad", "satd", "best_mode", "best_cost"):
-            assert np.array_equal(full[key], ref[key]), (wide, order, key)
+            assert np.array_equal(full[key], ref[key]), (knobs, key)
         for key in ("best_mode", "best_cost"):
-            assert np.array_equal(dec[key], ref[key]), (wide, order, "dec", key)
+            assert np.array_equal(dec[key], ref[key]), (knobs, "dec", key)
     cost, sad, satd = O.engine_search(frames[n - 1], filt, k, want_sad_satd=True)
     assert np.array_equal(ref["cost"][n - 1], cost)
     assert np.array_equal(ref["sad"][n - 1], sad) and np.array_equal(ref["satd"][n - 1], satd)

@@ -105,6 +105,10 @@ struct SearchArgs {
   // (read by the host after the search; only ever written when the contract is broken).
   uint32_t *status;
   int check_refs;
+  // 16-wave launches with the longest-first order and original references (pair mode,
+  // mip_search.hip pair_loop): the first `nonempty` queue positions hold the items with
+  // tasks, the rest only fills.  0: items one at a time.
+  uint32_t nonempty;
 };
 constexpr int kStatusOrig = 0, kStatusRefs = 1, kStatusWords = 4;
 constexpr uint32_t kAbove10Bits = 0xfc00fc00u;  // any of bits 10..15 in either half

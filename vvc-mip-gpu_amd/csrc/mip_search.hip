@@ -1430,8 +1430,8 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
 // taken after the current one instead; launches with fewer than MIP_PREFETCH_MIN_ITEMS items
 // per workgroup do not prefetch at all (1-frame launches measured -9 % with the prefetching
 // kernel).  The ALT lattice leaves no LDS for a second window.
-template <bool ALT, bool PF>
-constexpr int kOrgTiles = PF && !ALT ? 2 : 1;
+template <bool ALT, bool PF, int NW = kSearchWaves>
+constexpr int kOrgTiles = (PF || NW == kWideWaves) && !ALT ? 2 : 1;  // (16 waves: pair mode)
 constexpr int kCounterWords = 12;  // [parity]: next task, finished waves, item, item taken late;
                                    // [8]: chunks this workgroup has found empty (take_item)
 
@@ -1538,6 +1538,107 @@ __device__ __forceinline__ void stamp_item_start(uint64_t *clk) {
                          (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
 }
 
+// Two items' windows staged at once (pair mode): every thread's loads of both windows are in
+// flight before its first LDS store.  b = false: the second item is absent.
+template <int NT>
+__device__ __forceinline__ void stage_tiles2(uint16_t *dst0, const uint16_t *frame0, int x0, int y0, uint16_t *dst1,
+                                             const uint16_t *frame1, int x1, int y1, bool b, int width, int height,
+                                             uint32_t *status) {
+  const WindowStager<NT> s0(frame0, width, height, x0, y0, (int)threadIdx.x);
+  const WindowStager<NT> s1(frame1, width, height, x1, y1, (int)threadIdx.x);
+  constexpr int N = WindowStager<NT>::N;
+  uint2 v0[N], v1[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    if (s0.valid(k)) v0[k] = s0.load(k);
+    if (b && s1.valid(k)) v1[k] = s1.load(k);
+  }
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    if (s0.valid(k)) {
+      bits |= v0[k].x | v0[k].y;
+      s0.store(dst0, k, v0[k]);
+    }
+    if (b && s1.valid(k)) {
+      bits |= v1[k].x | v1[k].y;
+      s1.store(dst1, k, v1[k]);
+    }
+  }
+  flag_above_10_bits(bits, status, kStatusOrig);
+}
+
+// Pair mode (16-wave workgroups, one per CU; one-frame launches with original references and
+// the longest-first order, launch_search): a workgroup takes two items at once -- queue
+// positions p and E - 1 - p of the E items with tasks (SearchArgs::nonempty), a long one with
+// a short one -- stages both windows and lets its 16 waves take the two items' tasks from one
+// LDS counter (interleaved, so both lists' long tasks come first); the items without tasks
+// (last in the order: bottom quadrants) are fill-only and go along with pairs p, p + P, ...
+// Two items per CU run in ~150 us this way, against ~160 us one after the other.
+template <bool DEC>
+__device__ __forceinline__ void pair_loop(const SearchArgs &a, uint16_t *org_buf, const uint8_t *w, const uint8_t *zero,
+                                          uint8_t *waves, uint32_t *counters, int wave, int lane) {
+  const uint32_t ne = a.nonempty, npairs = (ne + 1) / 2;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      counters[0] = 0;
+      counters[1] = atomicAdd(a.queue, 1u);  // one queue chunk (launch_search)
+    }
+    __syncthreads();
+    const uint32_t p = counters[1];
+    if (p >= npairs) break;  // workgroup-uniform
+    const uint32_t i0 = p, i1 = ne - 1 - p;
+    const bool two = i1 != i0;
+    const ItemPos p0(a, i0), p1(a, i1);
+    const int vq0 = a.ctu_var[p0.ctu] * 4 + p0.quad, vq1 = a.ctu_var[p1.ctu] * 4 + p1.quad;
+    const int l0 = vq0 * a.slices + p0.slice, l1 = vq1 * a.slices + p1.slice;
+    const int tb0 = a.list_begin[l0], n0 = a.list_begin[l0 + 1] - tb0;
+    const int tb1 = a.list_begin[l1], n1 = two ? a.list_begin[l1 + 1] - tb1 : 0;
+    fill_unavailable<DEC>(a, p0.frame, p0.ctu, vq0, p0.slice);
+    if (two) fill_unavailable<DEC>(a, p1.frame, p1.ctu, vq1, p1.slice);
+    for (uint32_t e = ne + p; e < a.nitems; e += npairs) {  // fill-only items
+      const ItemPos pe(a, e);
+      fill_unavailable<DEC>(a, pe.frame, pe.ctu, a.ctu_var[pe.ctu] * 4 + pe.quad, pe.slice);
+    }
+    uint16_t *org0 = org_buf, *org1 = org_buf + kTileElems;
+    stage_tiles2<64 * kWideWaves>(org0, a.orig + (size_t)p0.frame * a.width * a.height, p0.fx0, p0.fy0, org1,
+                                  a.orig + (size_t)p1.frame * a.width * a.height, p1.fx0, p1.fy0, two, a.width,
+                                  a.height, a.status);
+    __syncthreads();
+    uint64_t *clk0 = a.wave_clock ? a.wave_clock + (size_t)i0 * kClockSlots : nullptr;
+    uint64_t *clk1 = a.wave_clock && two ? a.wave_clock + (size_t)i1 * kClockSlots : nullptr;
+    if (clk0 && threadIdx.x == 0) {
+      stamp_item_start(clk0);
+      if (clk1) stamp_item_start(clk1);
+    }
+    const int m = n0 < n1 ? n0 : n1;
+    for (;;) {
+      uint32_t tn = 0;
+      if (lane == 0) tn = atomicAdd(counters, 1u);
+      const int t = (int)__builtin_amdgcn_readfirstlane(tn);
+      if (t >= n0 + n1) break;
+      // tasks 0 .. 2m-1 alternate between the items (each list is longest first), then the
+      // rest of the longer list
+      const bool second = t < 2 * m ? (t & 1) != 0 : n1 > n0;
+      const int k = t < 2 * m ? t >> 1 : t - m;
+      const uint64_t c0 = clk0 ? __builtin_readcyclecounter() : 0;
+      const WaveTask task = a.tasks[(second ? tb1 : tb0) + k];
+      const Ctx x{&a, second ? org1 : org0, second ? org1 : org0, w, zero, waves + wave * kWaveBytes,
+                  second ? p1.ctu : p0.ctu, second ? p1.frame : p0.frame, second ? p1.fx0 : p0.fx0,
+                  second ? p1.fy0 : p0.fy0};
+      const RefTile<false> rt{x.ref};
+      dispatch_task<false, DEC>(x, rt, task, lane);
+      uint64_t *clk = second ? clk1 : clk0;
+      if (clk && lane == 0) {
+        if (k < kClockSlots - 3) clk[k] = __builtin_readcyclecounter() - c0;
+        atomicMax(reinterpret_cast<unsigned long long *>(clk + kClockSlots - 2),
+                  (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      }
+    }
+    __syncthreads();  // every wave is done with the windows and the counters
+  }
+}
+
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
 // NW: waves per workgroup (kSearchWaves; kWideWaves: one workgroup per CU, small launches)
 template <bool ALT, bool DEC, bool PF_, int NW>
@@ -1545,8 +1646,8 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = PF_ && !ALT && NW == kSearchWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles windows
-  uint16_t *lattice = org_buf + kOrgTiles<ALT, PF> * kTileElems;
-  uint8_t *w = smem + (kOrgTiles<ALT, PF> * kTileElems + (ALT ? kLatElems : 0)) * 2;
+  uint16_t *lattice = org_buf + kOrgTiles<ALT, PF, NW> * kTileElems;
+  uint8_t *w = smem + (kOrgTiles<ALT, PF, NW> * kTileElems + (ALT ? kLatElems : 0)) * 2;
   uint8_t *zero = w + kTableBytes;
   uint8_t *waves = zero + kZeroBytes;
   uint32_t *counters = reinterpret_cast<uint32_t *>(waves + NW * kWaveBytes);
@@ -1557,6 +1658,9 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
     reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 
+  if (NW == kWideWaves && !ALT && !PF && a.nonempty > 0) {  // uniform: pair mode
+    pair_loop<DEC>(a, org_buf, w, zero, waves, counters, wave, lane);
+  } else {
   // Persistent workgroups (as many as are resident) take items = (frame, CTU, quadrant,
   // slice) from a device-wide queue (take_item), in order: the hardware's static round-robin of
   // workgroups over XCDs and CUs cannot balance items of unequal cost (edge CTUs).
@@ -1684,6 +1788,7 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
     }
     if (PF) par ^= 1;  // (a loop-carried parity costs the ALT kernel ~30 VGPRs)
   }
+  }
   // The last workgroup to leave resets the queue's counters for the next launch that uses it
   // (the host never runs two launches on one pair at the same time).
   if (threadIdx.x == 0) {
@@ -1765,7 +1870,8 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
 }  // namespace
 
 size_t search_lds_bytes(bool alt, bool pf, int waves) {
-  return (size_t)((pf && !alt ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
+  const bool two = (pf || waves == kWideWaves) && !alt;  // kOrgTiles
+  return (size_t)((two ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
          (size_t)waves * kWaveBytes + kCounterWords * 4;
 }
 
@@ -1809,6 +1915,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
                  : (a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)resident ? (uint32_t)kQueueChunks : 1u);
   a.nframes = (uint32_t)nframes;
   if (a.chunks > 1 || a.ctu0 != 0 || a.nrange != a.nctus) a.order = nullptr;  // large or range launches
+  if (!wide || alt_refs || !a.order || a.chunks != 1 || a.nonempty > a.nitems) a.nonempty = 0;  // pair mode
   const char *env = getenv("MIPGPU_GROUPS");  // tuning knob: persistent grid size
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;

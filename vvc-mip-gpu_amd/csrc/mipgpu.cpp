@@ -519,6 +519,7 @@ struct mip_engine {
     // costs in that order (pick_work's makespan model).
     uint32_t *d_order = nullptr;
     std::vector<double> order_cost;
+    uint32_t nonempty = 0;  // items of a frame with tasks (original references): the first in d_order
   };
   std::vector<Work> work;
   // pick_work's choice per frame count for small launches (index into `work`), [wide]
@@ -907,6 +908,12 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
       std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
       ew.order_cost.resize(order.size());
       for (size_t i = 0; i < order.size(); i++) ew.order_cost[i] = cost[order[i]];
+      for (uint32_t it : order) {  // (the empty items cost kItemOverhead / 8: they come last)
+        const int c = (int)(it / per_ctu), g = (int)(it % per_ctu), q = g / sl, slc = g % sl;
+        const int l = (cv.of_ctu[kMapOrig][c] * 4 + q) * sl + slc;
+        if (wl.list_begin[l + 1] == wl.list_begin[l]) break;
+        ew.nonempty++;
+      }
       ALLOC(ew.d_order, order.size() * sizeof(uint32_t));
       if (hipMemcpy(ew.d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
         return cleanup(fail("uploading the item order failed"));
@@ -1023,6 +1030,9 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.status = e->d_status;
   a.check_refs = alt && caller_refs;
   a.order = lpt_order_enabled() ? work.d_order : nullptr;  // launch_search drops it for large / range launches
+  // pair mode of 16-wave launches (original references; launch_search checks the rest)
+  const char *pv = getenv("MIPGPU_PAIR");  // A/B knob: 0 = 16-wave launches take items one at a time
+  a.nonempty = work.wide && !alt && a.order && !(pv && *pv == '0') ? work.nonempty * (uint32_t)nframes : 0;
   // MIPGPU_WAVE_TIMING=file (profiling): per-task cycles appended to `file` (synchronous;
   // one binary record of uint64 [workgroup][wave][kClockSlots] per launch), and the task
   // lists to `file`.tasks once.
