@@ -109,3 +109,21 @@ def test_build_id_names_the_sources(lib):
     assert bid.startswith("src:") and " git:" in bid, bid
     want = subprocess.check_output(["make", "-s", "-C", os.path.join(REPO, "vvc-mip-gpu_amd"), "build-id"]).decode()
     assert mipgpu.source_id(bid) == mipgpu.source_id(want.strip())
+
+
+@pytest.mark.parametrize("knob", ["MIPGPU_NO_PAIRS", "MIPGPU_SHAPE_FILTER"])
+def test_wrong_result_knobs_are_refused_by_the_release_library(lib, monkeypatch, knob):
+    """Profiling knobs that make wrong tables by design (MIPGPU_NO_PAIRS: no mode pair searched;
+    MIPGPU_SHAPE_FILTER: a subset of the shapes) are honoured only by A/B builds with
+    -DMIPGPU_PROFILING_KNOBS (named in the build ID); the release library refuses to create an
+    engine while one is set -- before any HIP call -- instead of returning silently wrong
+    costs through the C ABI, the Python binding or the CLI."""
+    assert "knobs:" not in mipgpu.build_id()
+    monkeypatch.setenv(knob, "1")
+    o = mipgpu._Opts()
+    lib.mip_opts_default(ctypes.byref(o))
+    e = ctypes.c_void_p()
+    assert lib.mip_engine_create(0, 256, 136, ctypes.byref(o), ctypes.byref(e)) != 0 and not e.value
+    assert knob.encode() in lib.mip_last_error() and b"profiling knob" in lib.mip_last_error()
+    with pytest.raises(mipgpu.MipError, match="profiling knob"):
+        mipgpu.MipEngine(256, 136)

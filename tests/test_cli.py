@@ -319,3 +319,17 @@ def test_samples_above_10_bits_are_refused(gpu_available, tmp_path):
     frames.astype("<u2").tofile(tmp_path / "in.u16")
     r = run(["-f", str(N), "-s", f"{W}x{H}", "-o", str(tmp_path / "in.u16"), "-l", str(tmp_path / "o2")])
     assert r.returncode == 1 and "above 10 bits" in r.stdout, r.stdout + r.stderr
+
+
+@needs_cli
+def test_wrong_result_knob_stops_the_cli(tmp_path):
+    """`MIPGPU_NO_PAIRS=1 mipgpu_cli ...` (a profiling knob of A/B builds: no mode pair
+    searched) exits with an error naming the knob and writes no cost log (CPU: the release
+    library refuses the knob before touching the GPU)."""
+    frames = synth_frames(128, 128, 1, 0xC18, 0)
+    write_csv(tmp_path / "in.csv", frames)
+    env = dict(os.environ, MIPGPU_NO_PAIRS="1")
+    r = subprocess.run([CLI, "-f", "1", "-s", "128x128", "-o", str(tmp_path / "in.csv"), "-l", str(tmp_path / "o")],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "MIPGPU_NO_PAIRS" in r.stdout + r.stderr, r.stdout + r.stderr
+    assert not (tmp_path / "o.csv").exists()

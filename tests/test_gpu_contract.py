@@ -90,3 +90,48 @@ def test_prefetching_launch_checks_the_prefetched_windows(gpu_available):
         batch[29, 500, 700] = 15
         eng.search_device(batch, costs=costs)
         eng.check_input()
+
+
+def test_contract_error_belongs_to_the_call_that_searched_it(gpu_available):
+    """Per-call status (mip_wait reads only its own call's status set): three calls in flight,
+    only the second holds a sample above 1023.  Its ticket fails -- whichever ticket is waited
+    for first -- and the good calls' tickets succeed with the oracle's tables."""
+    w, h = 256, 136
+    frames = synth_frames(w, h, 3, 0xE15, 0)
+    bad = frames[1:2].copy()
+    bad[0, 70, 30] = 2047
+    with MipEngine(w, h, max_batch=1) as eng:
+        for order in ((2, 0, 1), (0, 1, 2), (1, 2, 0)):
+            t = [eng.search_async(frames[0:1]), eng.search_async(bad), eng.search_async(frames[2:3])]
+            for i in order:
+                if i == 1:
+                    with pytest.raises(MipError, match="above 10 bits"):
+                        eng.wait(t[i])
+                else:
+                    out = eng.wait(t[i])
+                    assert np.array_equal(out["cost"][0], O.search(frames[i])), (order, i)
+
+
+def test_caller_reference_check_at_the_last_columns(gpu_available):
+    """Caller-supplied references: frame columns W-2, W-1 are exempt from the 10-bit check only
+    at widths that are not multiples of 128 (their CUs go to the exact 32-bit fixup kernel);
+    at W = 256 a bad sample there is refused like anywhere else, at W = 264 it is searched
+    exactly (oracle)."""
+    frame256 = synth_frame(256, 136, 0xE16, 0)
+    with MipEngine(256, 136) as eng:
+        for y, x in ((63, 255), (63, 254), (63, 253)):  # row 63: the top row of CUs at y = 64
+            refs = synth_frame(256, 136, 0xE17, 1)
+            refs[y, x] = 1500
+            with pytest.raises(MipError, match="reference samples above 10 bits"):
+                eng.search(frame256, refs=refs)
+    # (row 100 is no reference row, but column 263 = 4 * 66 - 1 is a left reference column)
+    frame264 = synth_frame(264, 136, 0xE18, 0)
+    with MipEngine(264, 136) as eng:
+        for y, x in ((63, 263), (63, 262), (100, 263)):
+            refs = synth_frame(264, 136, 0xE19, 1)
+            refs[y, x] = 1500
+            assert np.array_equal(eng.search(frame264, refs=refs)["cost"][0], O.search(frame264, refs)), (y, x)
+        refs = synth_frame(264, 136, 0xE19, 1)
+        refs[63, 261] = 1500  # column W-3: checked at every width
+        with pytest.raises(MipError, match="reference samples above 10 bits"):
+            eng.search(frame264, refs=refs)

@@ -258,11 +258,12 @@ def test_extreme_content_clipping(gpu_available, pattern):
 def test_8k_alt_int_whole_table(gpu_available):
     """BASELINE configs[4]: one 7680x4320 frame per GPU with alternative references
     (filterFrame_2d_int_quarterCtu, KernelIdx 0), "integer bit-exact at 8K".  The reference
-    itself cannot run 8K -- its int32 reduced-prediction index overflows (2040 CTUs x
-    2 231 296 entries > 2^31, intra.cl:519-537) -- so the judge is the oracle, pinned to the
-    reference's kernels at 416x240 .. 4K (tests/golden): the whole filtered frame and the
-    WHOLE cost table (all 2040 CTUs, 199.6 M entries) must be bit-identical, and the
-    decisions-only path must give the table's argmin."""
+    cannot search the whole frame in one run -- its int32 reduced-prediction index overflows
+    (2040 CTUs x 2 231 296 entries > 2^31, intra.cl:519-537) -- so it ran as overlapping
+    crops of <= 960 CTUs (tests/golden/c6_4320p_alt_int.json, tools/ref_golden_8k.py): the
+    whole filtered frame and the WHOLE cost table (all 2040 CTUs, 199.6 M entries) must equal
+    the oracle bit for bit and, on the entries the reference defines, the stitched reference
+    table; the decisions-only path must give the table's argmin."""
     w, h, filt = 7680, 4320, "filterFrame_2d_int_quarterCtu"
     frame = synth_frame(w, h, 0x8E, 1)
     with MipEngine(w, h, filter=filt, kernel_idx=0) as eng:
@@ -272,6 +273,16 @@ def test_8k_alt_int_whole_table(gpu_available):
     assert np.array_equal(got_refs, O.filter_frame(frame, filt, 0))
     want = O.engine_search(frame, filt, 0)
     assert np.array_equal(out["cost"][0], want)
+    if "c6_4320p_alt_int" in G.names():  # the reference's own kernels (stitched crops)
+        fx = G.load("c6_4320p_alt_int")
+        assert (fx["config"]["seed"], fx["config"]["kind"]) == (0x8E, 1)
+        _, und, mask = G.refs_and_mask(fx, frame[None], 0)
+        fr = fx["frames"][0]
+        assert G.sha(G.masked(out["cost"][0], mask)) == fr["cost_sha256"]
+        assert G.filtered_sha(got_refs, und) == fr["filtered_sha256"]
+        for ctu in map(int, fr["ctu_rows"]):
+            sl = slice(ctu * 97840, (ctu + 1) * 97840)
+            assert np.array_equal(G.masked(out["cost"][0][sl], mask[sl]), G.ctu_row(fx, 0, ctu)), ctu
     bm, bc = layout.best_modes(want, layout.num_ctus(w, h))
     assert np.array_equal(out["best_mode"][0], bm) and np.array_equal(out["best_cost"][0], bc)
     assert np.array_equal(dec["best_mode"][0], bm) and np.array_equal(dec["best_cost"][0], bc)
@@ -661,3 +672,44 @@ def test_small_launch_shapes_agree(gpu_available, monkeypatch, w, h, n, filt, k)
     cost, sad, satd = O.engine_search(frames[n - 1], filt, k, want_sad_satd=True)
     assert np.array_equal(ref["cost"][n - 1], cost)
     assert np.array_equal(ref["sad"][n - 1], sad) and np.array_equal(ref["satd"][n - 1], satd)
+
+
+@pytest.mark.parametrize("w,filt,k", [(264, None, 0), (256, "filterFrame_2d_float_5x5_quarterCtu", 2)])
+def test_per_frame_calls_triple_buffered(gpu_available, w, filt, k):
+    """The drop-in's per-frame loop (main.cpp:678-1241 searches one frame per iteration):
+    default options (max_batch 1: three one-frame buffer slots), ten asynchronous one-frame
+    calls in flight at once with mixed outputs -- full table + decisions, decisions only,
+    caller references, page-locked and pageable buffers -- each equal to the oracle."""
+    from mipgpu import pinned_empty
+    h = 136
+    frames = synth_frames(w, h, 10, 0xF1A, 0)
+    refs = synth_frames(w, h, 10, 0xF1B, 0)
+    nct = layout.num_ctus(w, h)
+    kinds = ["full", "dec", "refs", "pinned_dec", "full", "refs_dec", "dec", "pinned_full", "full", "dec"]
+    with MipEngine(w, h, filter=filt, kernel_idx=k) as eng:
+        assert eng.max_batch == 1
+        tickets = []
+        for i, kind in enumerate(kinds):
+            f = frames[i:i + 1]
+            if kind.startswith("pinned"):
+                pf = pinned_empty(f.shape, np.uint16)
+                pf[:] = f
+                f = pf
+            r = refs[i:i + 1] if kind.startswith("refs") else None
+            if kind.endswith("dec"):
+                tickets.append(eng.search_async(f, refs=r, costs=False, best=True))
+            else:
+                tickets.append(eng.search_async(f, refs=r, best=True))
+        outs = [eng.wait(t) for t in tickets]
+    for i, (kind, o) in enumerate(zip(kinds, outs)):
+        if kind.startswith("refs"):
+            oc = O.search(frames[i], refs[i])
+        elif filt is None:
+            oc = O.search(frames[i])
+        else:
+            oc = O.search(frames[i], O.filter_frame(frames[i], filt, k))
+        bm, bc = layout.best_modes(oc, nct)
+        if "cost" in o:
+            assert np.array_equal(o["cost"][0], oc), (i, kind)
+        assert np.array_equal(o["best_mode"][0], bm), (i, kind)
+        assert np.array_equal(o["best_cost"][0], bc), (i, kind)

@@ -1,10 +1,24 @@
 #!/bin/bash
-# Build an A/B variant of libmipgpu.so with extra compiler flags for the search kernel:
+# Build an A/B variant of libmipgpu.so with extra compiler flags for every engine source:
 #   tools/build_variant.sh OUT.so [extra hipcc flags...]
+# e.g. the profiling build that honours MIPGPU_SHAPE_FILTER / MIPGPU_NO_PAIRS (wrong tables
+# by design; the release library refuses them):
+#   tools/build_variant.sh tools/bin/libmipgpu_prof.so -DMIPGPU_PROFILING_KNOBS
+# The variant's build ID names the extra flags (knobs:...), so bench.py and profiles/ never
+# take it for the release library.
 set -euo pipefail
 cd "$(dirname "$0")/../vvc-mip-gpu_amd"
 out=$1; shift
+case "$out" in /*) ;; *) out="$OLDPWD/$out" ;; esac
+mkdir -p "$(dirname "$out")"
 tmp=$(mktemp -d)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc "$@" -c -o $tmp/mip_search.o csrc/mip_search.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OLDPWD/$out" $tmp/mip_search.o build/mip_filter.o build/mip_fixup.o build/mipgpu.o
-rm -rf $tmp
+trap 'rm -rf "$tmp"' EXIT
+id="$(make -s KNOBS="$*" build-id)"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc $*"
+for s in mip_search mip_filter mip_fixup; do
+  /opt/rocm/bin/hipcc $F -c -o "$tmp/$s.o" "csrc/$s.hip" &
+done
+/opt/rocm/bin/hipcc $F "-DMIPGPU_BUILD_ID=\"$id\"" -c -o "$tmp/mipgpu.o" csrc/mipgpu.cpp &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$out" "$tmp"/*.o
+echo "built $out ($id)"

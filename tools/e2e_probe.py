@@ -1,7 +1,22 @@
 #!/usr/bin/env python3
-"""Host-buffer pipeline probe: decisions-only and full-cost end-to-end rates of
-mip_search_frames for a few batch sizes (run under rocprofv3 --kernel-trace
---memory-copy-trace to see the overlap of H2D, search, best-mode and D2H)."""
+"""Host-buffer pipeline probe: end-to-end rates of mip_search_frames_async / mip_wait for
+given call shapes (run under rocprofv3 --kernel-trace --memory-copy-trace to see the overlap
+of H2D, filter, search and D2H; tools/trace_timeline.py summarises such a trace).
+
+    python tools/e2e_probe.py [--calls 8] [--reps 3] CASE [CASE ...]
+
+CASE = FRAMES:OUT:HOST[:FILTER:KIDX][:mb=MAX_BATCH]
+  FRAMES  frames per call (1080p unless --width/--height)
+  OUT     dec (per-CU best mode + cost only) | full (int32 cost table)
+  HOST    pinned (mip_host_alloc buffers) | pageable (malloc'd numpy arrays)
+  FILTER  reference filter name (alternative references, engine filter), KIDX its KernelIdx
+  mb=M    engine max_batch (default FRAMES: the drop-in's per-call engine, as bench.py's
+          config sweep creates it)
+Each case: an engine, one warm-up call, then `reps` rounds of `calls` asynchronous calls
+queued back to back and one wait for the last; prints one JSON line per case (median rate,
+all rates).  Cases are separated by 0.2 s of idle time (trace segments)."""
+import argparse
+import json
 import os
 import sys
 import time
@@ -13,18 +28,56 @@ import numpy as np  # noqa: E402
 from mipgpu import MipEngine, pinned_empty  # noqa: E402
 from mipgpu.synth import synth_frames  # noqa: E402
 
-W, H = 1920, 1080
-for B in [int(x) for x in (sys.argv[1:] or ["32"])]:
-    host = synth_frames(W, H, min(B, 8), 0x1080, 0)
-    hp = pinned_empty((B, H, W), np.uint16)
-    for i in range(B):
-        hp[i] = host[i % host.shape[0]]
-    with MipEngine(W, H, max_batch=B) as eng:
-        dout = {"best_mode": pinned_empty((B, eng.cus_per_frame), np.uint8),
-                "best_cost": pinned_empty((B, eng.cus_per_frame), np.int32)}
-        eng.search(hp, costs=False, best=True, out=dout)
-        t0 = time.perf_counter()
-        for _ in range(3):
-            eng.search(hp, costs=False, best=True, out=dout)
-        dec = 3 * B / (time.perf_counter() - t0)
-        print("B=%d decisions %.1f frames/s" % (B, dec), flush=True)
+
+def parse(case):
+    parts = case.split(":")
+    mb = None
+    if parts[-1].startswith("mb="):
+        mb = int(parts.pop()[3:])
+    f, out, host = int(parts[0]), parts[1], parts[2]
+    flt = parts[3] if len(parts) > 3 else None
+    kidx = int(parts[4]) if len(parts) > 4 else 0
+    assert out in ("dec", "full") and host in ("pinned", "pageable"), case
+    return f, out, host, flt, kidx, mb or f
+
+
+def run(case, W, H, calls, reps):
+    F, out, host, flt, kidx, mb = parse(case)
+    src = synth_frames(W, H, min(F, 4), 0x1080, 0)
+    alloc = (lambda shape, dt: pinned_empty(shape, dt)) if host == "pinned" else (lambda shape, dt: np.zeros(shape, dt))
+    frames = alloc((F, H, W), np.uint16)
+    for i in range(F):
+        frames[i] = src[i % src.shape[0]]
+    with MipEngine(W, H, max_batch=mb, filter=flt, kernel_idx=kidx) as eng:
+        if out == "dec":
+            o = {"best_mode": alloc((F, eng.cus_per_frame), np.uint8), "best_cost": alloc((F, eng.cus_per_frame), np.int32)}
+            kw = dict(costs=False, best=True, out=o)
+        else:
+            o = {"cost": alloc((F, eng.costs_per_frame), np.int32)}
+            kw = dict(out=o)
+        eng.search(frames, **kw)
+        rates = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            eng.wait([eng.search_async(frames, **kw) for _ in range(calls)][-1])
+            rates.append(calls * F / (time.perf_counter() - t0))
+    return {"case": case, "frames_per_call": F, "out": out, "host": host, "filter": flt, "kernel_idx": kidx,
+            "max_batch": mb, "calls": calls, "fps": round(float(np.median(rates)), 1),
+            "fps_all": [round(r, 1) for r in rates]}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("cases", nargs="+")
+    ap.add_argument("--calls", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    a = ap.parse_args()
+    for c in a.cases:
+        print(json.dumps(run(c, a.width, a.height, a.calls, a.reps)), flush=True)
+        time.sleep(0.2)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,10 +1,18 @@
 #!/usr/bin/env python3
-"""Time the fused search per CU-size class (MIPGPU_SHAPE_FILTER) on 1080p frames."""
+"""Time the fused search per CU-size class (MIPGPU_SHAPE_FILTER) on 1080p frames.
+
+MIPGPU_SHAPE_FILTER is a profiling knob honoured only by a profiling build
+(tools/build_variant.sh tools/bin/libmipgpu_prof.so -DMIPGPU_PROFILING_KNOBS); this script
+loads that build (MIPGPU_LIB) -- the release library refuses the knob."""
 import json
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("MIPGPU_LIB", os.path.join(REPO, "tools", "bin", "libmipgpu_prof.so"))
+if not os.path.exists(os.environ["MIPGPU_LIB"]):
+    sys.exit("%s missing: build it with tools/build_variant.sh tools/bin/libmipgpu_prof.so -DMIPGPU_PROFILING_KNOBS"
+             % os.environ["MIPGPU_LIB"])
 sys.path.insert(0, os.path.join(REPO, "vvc-mip-gpu_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -1383,7 +1383,9 @@ struct ItemPos {
 // Stage the reference lattice (ALT): rows 4i-1 (columns -4..63), columns 4i-1 (rows -1..63),
 // by linear index like the window (frame_chunk).
 // check: caller-supplied references (SearchArgs::check_refs) must be 10-bit too, except frame
-// columns W-2, W-1, whose CUs the exact fixup kernel searches (mipgpu.cpp reads_last_columns).
+// columns W-2, W-1 at widths that are not multiples of 128, whose CUs the exact fixup kernel
+// searches (mipgpu.cpp ctu_variants / reads_last_columns).  Samples are addressed linearly,
+// so a chunk's frame column is its x modulo the width.
 template <int NT>
 __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
                                               int x0, int y0, bool check, uint32_t *status) {
@@ -1404,18 +1406,28 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
     cv[k] = (fy >= 0 && fx >= 0 && li < width * height) ? frame[li] : 0;
   }
   uint32_t bits = 0;
+  const bool exempt_last = width % 128 != 0;  // fixup CUs exist (columns W-2, W-1)
+  auto frame_col = [&](int fx) { return fx < width ? fx : fx % width; };  // fx >= 0
 #pragma unroll
   for (int k = 0; k < NRL; k++) {
     const int i = min((int)threadIdx.x + NT * k, NR - 1), row = i / kChunks, ch = i - row * kChunks;
     *reinterpret_cast<uint2 *>(dst + row * kLatRowPitch + 4 * ch) = rv[k];
-    if (check && x0 - kColOff + 4 * ch != width - 4) bits |= rv[k].x | rv[k].y;
+    if (check) {
+      // .y holds the chunk's columns c+2, c+3: W-2, W-1 when c == W-4
+      const int fx = x0 - kColOff + 4 * ch;
+      const bool skip_y = exempt_last && fx >= 0 && frame_col(fx) == width - 4;
+      bits |= rv[k].x | (skip_y ? 0u : rv[k].y);
+    }
   }
   uint16_t *cols = dst + 16 * kLatRowPitch;
 #pragma unroll
   for (int k = 0; k < NCL; k++) {
     const int i = min((int)threadIdx.x + NT * k, NC - 1), col = i / 65, yy = i - col * 65;
     cols[col * kLatColPitch + yy] = cv[k];
-    if (check && x0 + 4 * col - 1 != width - 1) bits |= cv[k];
+    if (check) {
+      const int fx = x0 + 4 * col - 1;  // = 3 mod 4: only column W-1 can be exempt
+      if (!(exempt_last && fx >= 0 && frame_col(fx) == width - 1)) bits |= cv[k];
+    }
   }
   if (check) flag_above_10_bits(bits, status, kStatusRefs);
 }

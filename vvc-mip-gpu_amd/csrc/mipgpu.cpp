@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -129,7 +130,19 @@ struct WorkLists {
   int max_split = 0;
 };
 
+// Profiling knobs that give wrong tables by design (MIPGPU_SHAPE_FILTER, MIPGPU_NO_PAIRS) are
+// honoured only by A/B builds made with KNOBS=-DMIPGPU_PROFILING_KNOBS (the option enters the
+// build ID, mip_build_id()); a release build refuses to create an engine while they are set
+// (mip_engine_create), so no caller -- CLI, C ABI, Python -- gets a silently wrong table.
+#ifdef MIPGPU_PROFILING_KNOBS
+constexpr bool kProfilingKnobs = true;
+#else
+constexpr bool kProfilingKnobs = false;
+#endif
+const char *const kWrongResultKnobs[] = {"MIPGPU_SHAPE_FILTER", "MIPGPU_NO_PAIRS"};
+
 bool shape_selected(int s) {
+  if (!kProfilingKnobs) return true;
   const char *flt = getenv("MIPGPU_SHAPE_FILTER");
   if (!flt || !*flt) return true;
   for (const char *p = flt; *p;) {
@@ -158,7 +171,7 @@ bool transpose_wide() {
 // MIPGPU_NO_PAIRS=1 (profiling knob): tasks keep their prologue but search no mode pair.
 bool no_pairs() {
   const char *e = getenv("MIPGPU_NO_PAIRS");
-  return e && *e == '1';
+  return kProfilingKnobs && e && *e == '1';
 }
 
 // Estimated VALU instructions per lane for one mode pair of a task of `ncu` CUs.
@@ -477,7 +490,14 @@ struct mip_engine {
   // downloads; per buffer slot, events order upload -> compute -> download and a slot's
   // reuse after its previous chunk (see mip_search_frames).
   hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+  // Buffer slots of the host pipeline: hp_slots regions of hp_cap frames each in the engine
+  // buffers (d_frames, d_refs, d_costs, ...).  Large engines (max_batch >= 16): 4 slots of a
+  // quarter of max_batch; small ones: 3 slots of max_batch frames (triple buffering, so that a
+  // caller searching one frame per call -- the reference's per-frame loop with BUFFER_SLOTS 2,
+  // main.cpp:886-898, main_aux_functions.h:5, 617 -- overlaps frame k+1's upload and frame
+  // k-1's download with frame k's search).
   static constexpr int kHostSlots = 4;
+  int hp_slots = 0, hp_cap = 0, hp_frames = 0;  // hp_frames: frames of the engine buffers
   hipEvent_t slot_up[kHostSlots] = {}, slot_comp[kHostSlots] = {}, slot_down[kHostSlots] = {};
   // Chunks run through the slots in one global sequence across host-API calls, so that
   // asynchronous calls (mip_search_frames_async) keep the pipeline full; call k completes
@@ -522,8 +542,9 @@ struct mip_engine {
     uint32_t nonempty = 0;  // items of a frame with tasks (original references): the first in d_order
   };
   std::vector<Work> work;
-  // pick_work's choice per frame count for small launches (index into `work`), [wide]
-  std::vector<int> small_choice[2];
+  // pick_work's choice per frame count for small launches (index into `work`), [alt][wide]
+  // (the two reference modes have their own resident grids)
+  std::vector<int> small_choice[2][2];
   uint8_t *d_tables = nullptr;
   uint8_t *d_ctu_var[kMaps] = {};           // [map][nctus] CTU variant (ctu_variants: orig /
                                             // caller refs / engine-filtered refs)
@@ -556,8 +577,15 @@ struct mip_engine {
   QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this}};
   // Input contract (10-bit samples): status words the search kernel sets when it stages a
   // sample above 1023 (SearchArgs::status), in page-locked host memory mapped into the
-  // device; checked and cleared by check_status.
+  // device.  One set of kStatusWords per host-API call (call c: set (c - 1) % kCallRing) and
+  // one for the device API (set kCallRing), so that a violation is reported for the call
+  // that searched the frame: mip_wait(c) reads call c's set (harvest_status), the device API
+  // its own set (check_device_status).  status_harvested: calls <= it have had their set
+  // read and cleared; call_errors: the flags of harvested calls not yet reported (ticket ->
+  // 1 = frame samples, 2 = reference samples).
   uint32_t *h_status = nullptr, *d_status = nullptr;
+  uint64_t status_harvested = 0;
+  std::map<uint64_t, uint32_t> call_errors;
 };
 
 namespace {
@@ -624,7 +652,7 @@ const mip_engine::Work &pick_work(mip_engine *e, int nframes, int nrange, bool a
     return *best;
   }
   const bool wide = wide_launch(items1, e->resident_wide[alt ? 1 : 0]);
-  std::vector<int> &cache = e->small_choice[wide ? 1 : 0];
+  std::vector<int> &cache = e->small_choice[alt ? 1 : 0][wide ? 1 : 0];
   if ((int)cache.size() <= nframes) cache.resize(nframes + 1, -1);
   int &ch = cache[nframes];
   if (ch < 0) {
@@ -646,14 +674,50 @@ const mip_engine::Work &pick_work(mip_engine *e, int nframes, int nrange, bool a
 // samples into unsigned short and its kernels take short* (main.cpp:364-384, intra.cl:17,
 // 545), with 10-bit constants throughout (constants.cl:22-23, valueDC = 512, clip 1023);
 // this engine's packed 16-bit / f16 arithmetic is exact for 10-bit samples only.
-static int check_status(mip_engine *e) {
-  volatile uint32_t *st = e->h_status;
-  if (!st || !(st[mipgpu::kStatusOrig] | st[mipgpu::kStatusRefs])) return 0;
-  const bool orig = st[mipgpu::kStatusOrig] != 0;
-  st[mipgpu::kStatusOrig] = 0;
-  st[mipgpu::kStatusRefs] = 0;
-  return fail("input contract: %s samples above 10 bits (> 1023) in a frame searched by this engine; its costs are "
-              "not valid (samples must be 10-bit values)", orig ? "frame" : "reference");
+static uint32_t *status_set(mip_engine *e, int set) { return e->h_status + (size_t)set * mipgpu::kStatusWords; }
+
+// Read and clear a status set: 0, or 1 (frame samples) | 2 (reference samples).
+static uint32_t take_status(mip_engine *e, int set) {
+  volatile uint32_t *st = status_set(e, set);
+  const uint32_t f = (st[mipgpu::kStatusOrig] ? 1u : 0u) | (st[mipgpu::kStatusRefs] ? 2u : 0u);
+  if (f) {
+    st[mipgpu::kStatusOrig] = 0;
+    st[mipgpu::kStatusRefs] = 0;
+  }
+  return f;
+}
+
+static int contract_error(uint32_t flags, const char *what) {
+  return fail("input contract: %s samples above 10 bits (> 1023) in a frame searched by %s; its costs are not valid "
+              "(samples must be 10-bit values)", (flags & 1) ? "frame" : "reference", what);
+}
+
+// Device API: the searches issued since the last check (asynchronous: reported by
+// mip_check_input or the next device-API search call).
+static int check_device_status(mip_engine *e) {
+  const uint32_t f = take_status(e, mip_engine::kCallRing);
+  return f ? contract_error(f, "a device-API search of this engine") : 0;
+}
+
+// Device pointers of the status sets the kernels mark.
+static uint32_t *device_status(mip_engine *e) { return e->d_status + (size_t)mip_engine::kCallRing * mipgpu::kStatusWords; }
+static uint32_t *call_status(mip_engine *e, uint64_t call) {
+  return e->d_status + (size_t)((call - 1) % mip_engine::kCallRing) * mipgpu::kStatusWords;
+}
+
+// Host API: move the status sets of the completed calls (status_harvested, upto] into
+// call_errors (only calls that saw a violation are kept; at most kMaxCallErrors of them).
+// Every call <= upto must have completed.
+static void harvest_status(mip_engine *e, uint64_t upto) {
+  constexpr size_t kMaxCallErrors = 4096;
+  for (uint64_t c = e->status_harvested + 1; c <= upto; c++) {
+    const uint32_t f = take_status(e, (int)((c - 1) % mip_engine::kCallRing));
+    if (f) {
+      if (e->call_errors.size() >= kMaxCallErrors) e->call_errors.erase(e->call_errors.begin());
+      e->call_errors[c] = f;
+    }
+  }
+  if (upto > e->status_harvested) e->status_harvested = upto;
 }
 
 // Host-API calls (synchronous) overwrite engine scratch: order them after the device-API
@@ -792,6 +856,11 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   if (o.filter != MIP_FILTER_NONE) {
     if (!filter_valid(o.filter, o.kernel_idx)) return fail("invalid filter %d / kernel_idx %d", o.filter, o.kernel_idx);
   }
+  if (!kProfilingKnobs)
+    for (const char *k : kWrongResultKnobs)
+      if (const char *v = getenv(k); v && *v)
+        return fail("%s is set: a profiling knob that makes wrong cost tables by design, honoured only by A/B builds "
+                    "(make KNOBS=-DMIPGPU_PROFILING_KNOBS); this release build refuses to run with it -- unset it", k);
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail("device %d out of range (%d devices)", device, ndev);
@@ -804,7 +873,11 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   e->nctus = mip_num_ctus(width, height);
   e->ctu_cols = (width + 127) / 128;
   e->opts = o;
-  const size_t fs = (size_t)width * height, nb = (size_t)o.max_batch;
+  // host pipeline slots (see mip_engine::hp_slots); the engine buffers hold all of them
+  e->hp_slots = o.max_batch >= 16 ? 4 : 3;
+  e->hp_cap = o.max_batch >= 16 ? o.max_batch / 4 : o.max_batch;
+  e->hp_frames = std::max(o.max_batch, e->hp_slots * e->hp_cap);
+  const size_t fs = (size_t)width * height, nb = (size_t)e->hp_frames;
   const size_t ncost = nb * e->nctus * MIP_COSTS_PER_CTU, ncu = nb * e->nctus * MIP_CUS_PER_CTU;
   auto cleanup = [&](int rc) { mip_engine_destroy(e); return rc; };
 #define ALLOC(ptr, bytes)                                                               \
@@ -836,10 +909,10 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     return cleanup(fail("hipMemset failed"));
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
-  if (hipHostMalloc((void **)&e->h_status, mipgpu::kStatusWords * sizeof(uint32_t),
-                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+  const size_t status_bytes = (size_t)(mip_engine::kCallRing + 1) * mipgpu::kStatusWords * sizeof(uint32_t);
+  if (hipHostMalloc((void **)&e->h_status, status_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
     return cleanup(fail("hipHostMalloc (status words) failed"));
-  memset(e->h_status, 0, mipgpu::kStatusWords * sizeof(uint32_t));
+  memset(e->h_status, 0, status_bytes);
   if (hipHostGetDevicePointer((void **)&e->d_status, e->h_status, 0) != hipSuccess || !e->d_status)
     return cleanup(fail("hipHostGetDevicePointer (status words) failed"));
   if (hipEventCreateWithFlags(&e->refs_done, hipEventDisableTiming) != hipSuccess)
@@ -969,8 +1042,8 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
 // defined > 10-bit outputs at the last columns go to the fixup kernel).
 static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
-                              int32_t *d_best_cost, hipStream_t s, bool caller_refs, int ctu0 = 0,
-                              int nrange = -1) {
+                              int32_t *d_best_cost, hipStream_t s, bool caller_refs, uint32_t *d_status,
+                              int ctu0 = 0, int nrange = -1) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
   // Decisions only (no cost table): the search writes each CU's decision into d_best /
   // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
@@ -1027,7 +1100,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.ctu0 = ctu0;
   a.nrange = nrange;
   a.slices = work.slices;
-  a.status = e->d_status;
+  a.status = d_status;  // the calling API's status set (mip_engine::h_status)
   a.check_refs = alt && caller_refs;
   a.order = lpt_order_enabled() ? work.d_order : nullptr;  // launch_search drops it for large / range launches
   // pair mode of 16-wave launches (original references; launch_search checks the rest)
@@ -1097,17 +1170,17 @@ int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d
                       int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best_mode,
                       int32_t *d_best_cost, void *stream) {
   if (!e) return fail("engine is NULL");
-  if (check_status(e) != 0) return -1;
+  if (check_device_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, d_best_mode, d_best_cost,
-                            (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames);
+                            (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames, device_status(e));
 }
 
 int mip_check_input(mip_engine *e, void *stream) {
   if (!e) return fail("engine is NULL");
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-  return check_status(e);
+  return check_device_status(e);
 }
 
 int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
@@ -1117,10 +1190,10 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
   if (!d_costs) return fail("d_costs is NULL");
   // an empty range (more CTU-row bands than CTU rows, mipgpu.split) is a successful no-op
   if (ctu_begin == ctu_end && ctu_begin >= 0 && ctu_end <= e->nctus) return 0;
-  if (check_status(e) != 0) return -1;
+  if (check_device_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, nullptr, nullptr,
-                            (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames, ctu_begin,
+                            (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames, device_status(e), ctu_begin,
                             ctu_end - ctu_begin);
 }
 
@@ -1150,10 +1223,16 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
   if (!e || !frames || nframes < 1 || !ticket) return fail("bad search arguments");
   *ticket = 0;
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
-  if (check_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
+  const uint64_t next = e->host_calls + 1;
+  // call `next` marks status set (next - 1) % kCallRing: the call that used it before (more
+  // than kCallRing calls in flight) must have completed and been harvested first
+  if (next > (uint64_t)mip_engine::kCallRing && e->status_harvested < next - mip_engine::kCallRing) {
+    HIP_TRY(hipEventSynchronize(e->call_done[(next - 1) % mip_engine::kCallRing]));
+    harvest_status(e, next - mip_engine::kCallRing);
+  }
   const int rc = search_frames_chunks(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out,
-                                      sad_out, satd_out, e->host_calls + 1);
+                                      sad_out, satd_out, next);
   // Also after a failure part-way through the chunks: the chunks already queued on the
   // upload / search streams are covered by host_done (later device-API searches that filter
   // into the engine's reference scratch wait for it) and by this call's completion event.
@@ -1168,6 +1247,7 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
     // staged downloads of the calls before this one complete normally; this call's are dropped
     (void)e->stage.drain(e->host_calls);
     e->stage.abandon();
+    (void)take_status(e, (int)((next - 1) % mip_engine::kCallRing));  // the failed call's chunks: no ticket
     g_err = err;
     return rc;
   }
@@ -1185,27 +1265,38 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
                                 int32_t *satd_out, uint64_t call) {
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
-    HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
+    HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
   if (wait_refs_readers(e) != 0) return -1;
   e->refs_pending = false;  // the waits above order every later use of the engine streams
   const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
-  // Chunks of `sb` frames rotate over `nslots` slots of the engine buffers (a quarter or a
-  // half of max_batch each) through a three-stream pipeline: stream2 uploads chunk k+1 while
-  // `stream` searches chunk k and stream3 downloads chunk k-1, so the copy engines (H2D and
-  // D2H) and the compute run concurrently and the search kernels keep the whole GPU.  Per
-  // slot: the upload waits until the previous chunk of the slot has been searched (its
-  // frames / refs are free), the search waits for the upload and for the previous download
-  // of the slot's outputs, the download waits for the search.  The chunk sequence (and so
-  // the slot rotation and these waits) continues across calls, so asynchronous calls queue
-  // behind each other without draining the pipeline.  Transfers run at DMA rate from
-  // page-locked host memory (mip_host_alloc); pageable buffers go through the engine's
-  // page-locked bounce ring (host_stage.h), their downloads finished by mip_wait.
-  const int nslots = e->opts.max_batch >= 16 ? 4 : (e->opts.max_batch >= 2 ? 2 : 1);
+  // Chunks of `sb` frames rotate over the engine's hp_slots buffer slots (mip_engine::hp_slots:
+  // 4 slots of a quarter of max_batch, or 3 slots of max_batch for engines below 16 frames)
+  // through a three-stream pipeline: stream2 uploads chunk k+1 while `stream` searches chunk k
+  // and stream3 downloads chunk k-1, so the copy engines (H2D and D2H) and the compute run
+  // concurrently and the search kernels keep the whole GPU.  Per slot: the upload waits until
+  // the previous chunk of the slot has been searched (its frames / refs are free), the search
+  // waits for the upload and for the previous download of the slot's outputs, the download
+  // waits for the search.  The chunk sequence (and so the slot rotation and these waits)
+  // continues across calls, so asynchronous calls queue behind each other without draining
+  // the pipeline -- with three slots even one-frame calls overlap (the reference's
+  // BUFFER_SLOTS 2 loop: frame curr+1's upload during frame curr's kernels, main.cpp:886-898,
+  // and a non-blocking read-back of slot curr % 2, main_aux_functions.h:617).  Transfers run
+  // at DMA rate from page-locked host memory (mip_host_alloc); pageable buffers go through the
+  // engine's page-locked bounce ring (host_stage.h), their downloads finished by mip_wait.
+  const int nslots = e->hp_slots;
   // a slot is a fixed region of slot_cap frames of the engine buffers (chunk sizes differ
   // between calls -- outputs requested, call length -- but a slot's region never moves, so
   // the per-slot events order every reuse of it)
-  const int slot_cap = e->opts.max_batch / nslots;
+  const int slot_cap = e->hp_cap;
   int sb = slot_cap;
+  // A call into an idle pipeline (nothing queued before it) is cut in two, so that its own
+  // upload, search and download overlap; calls queued behind others keep whole-call chunks
+  // (the overlap comes from the neighbouring calls, and larger launches are more efficient).
+  if (nslots == 3 && nframes >= 2) {
+    const bool idle = e->host_calls == 0 ||
+                      hipEventQuery(e->call_done[(e->host_calls - 1) % mip_engine::kCallRing]) == hipSuccess;
+    if (idle) sb = (nframes + 1) / 2;
+  }
   // Full tables to the host (PCIe-bound): chunks of at most ~1 GiB of downloads, so the
   // first download starts early and, for pageable outputs, the bounce ring's copy-out keeps
   // up (1080p, 8 calls of 128 frames: 96-frame chunks 831 frames/s pageable, 32-frame 892,
@@ -1225,22 +1316,31 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   const bool pin_satd = !satd_out || mipgpu::HostStage::pinned(satd_out);
   const bool pin_bm = !best_mode_out || mipgpu::HostStage::pinned(best_mode_out);
   const bool pin_bc = !best_cost_out || mipgpu::HostStage::pinned(best_cost_out);
-  // pageable outputs: a chunk's downloads fit the bounce ring beside the next chunk's
-  // uploads (host_stage.h kMaxChunkPieces), so enqueueing them never waits for the chunk's
-  // own search
-  const size_t pageable_down = (size_t)((pin_cost ? 0 : 1) + (pin_sad ? 0 : 1) + (pin_satd ? 0 : 1)) * cpf * 4 +
-                               (pin_bm ? 0 : upf) + (pin_bc ? 0 : upf * 4);
-  if (pageable_down) {
-    const size_t ring = (size_t)mipgpu::HostStage::kMaxChunkPieces * mipgpu::HostStage::kMaxPiece;
-    sb = std::max(1, std::min<int>(sb, (int)(ring / pageable_down)));
-  }
-  {  // equal chunks: a short last chunk would leave the search waiting for the next upload
+  auto equal_chunks = [&] {  // a short last chunk would leave the search waiting for the next upload
     const int nch = (nframes + sb - 1) / sb;
     sb = (nframes + nch - 1) / nch;
-  }
+  };
+  equal_chunks();
   if (!(pin_in && pin_cost && pin_sad && pin_satd && pin_bm && pin_bc)) {
     const size_t most = std::max({(size_t)sb * fs * 2, (size_t)sb * cpf * 4, (size_t)sb * upf * 4});
     HIP_TRY(e->stage.reserve(std::min<size_t>(most, mipgpu::HostStage::kMaxPiece)));
+    // Pageable transfers are cut into ring pieces per buffer: a chunk's downloads must fit
+    // the ring beside the next chunk's uploads (host_stage.h kMaxChunkPieces), else
+    // enqueueing them waits on the host for the chunk's own search.  Counted per buffer
+    // (each rounds up to whole pieces).
+    const size_t piece = e->stage.piece();
+    auto pieces = [&](bool pinned, size_t bytes_per_frame) -> int {
+      return pinned || !bytes_per_frame ? 0 : (int)(((size_t)sb * bytes_per_frame + piece - 1) / piece);
+    };
+    auto fits = [&] {
+      const int down_p = pieces(pin_cost, costs_out ? cpf * 4 : 0) + pieces(pin_sad, sad_out ? cpf * 4 : 0) +
+                         pieces(pin_satd, satd_out ? cpf * 4 : 0) + pieces(pin_bm, best_mode_out ? upf : 0) +
+                         pieces(pin_bc, best_cost_out ? upf * 4 : 0);
+      const int up_p = pieces(pin_in, fs * 2) * (refs_or_null ? 2 : 1);
+      return down_p <= mipgpu::HostStage::kMaxChunkPieces && up_p <= mipgpu::HostStage::kRing - mipgpu::HostStage::kMaxChunkPieces;
+    };
+    while (sb > 1 && !fits()) sb--;
+    equal_chunks();
   }
   // host <-> device copy on stream s: DMA from / to page-locked memory, else the bounce ring
   auto to_dev = [&](void *d, const void *h, size_t n, bool pinned) {
@@ -1296,7 +1396,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     uint8_t *d_best = best_mode_out ? e->d_best + fo * upf : nullptr;
     int32_t *d_best_cost = best_cost_out || decisions_only ? e->d_best_cost + fo * upf : nullptr;
     if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
-                           refs_or_null != nullptr) != 0)
+                           refs_or_null != nullptr, call_status(e, call)) != 0)
       return -1;
     HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     if (!any_out) continue;
@@ -1320,7 +1420,16 @@ int mip_wait(mip_engine *e, uint64_t ticket) {
   HIP_TRY(hipEventSynchronize(e->call_done[(ticket - 1) % mip_engine::kCallRing]));
   // pageable outputs: copy the call's staged downloads out (and everything queued before)
   HIP_TRY(e->stage.drain(ticket));
-  return check_status(e);
+  // input contract of this call only (every call <= ticket has completed: calls complete in
+  // order); the flags of earlier calls stay with their own tickets
+  harvest_status(e, ticket);
+  const auto it = e->call_errors.find(ticket);
+  if (it == e->call_errors.end()) return 0;
+  const uint32_t f = it->second;
+  e->call_errors.erase(it);
+  char what[64];
+  snprintf(what, sizeof what, "host-API call %llu of this engine", (unsigned long long)ticket);
+  return contract_error(f, what);
 }
 
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
@@ -1390,7 +1499,7 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
   if (!e || !frames || !out || nframes < 1) return fail("bad filter arguments");
   HIP_TRY(hipSetDevice(e->device));
   const size_t fs = (size_t)e->width * e->height;
-  if (!e->d_refs) HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->opts.max_batch * 2));
+  if (!e->d_refs) HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
   if (wait_refs_readers(e) != 0) return -1;
   // asynchronous host searches still in flight use d_frames / d_refs: let them finish
   HIP_TRY(hipStreamSynchronize(e->stream2));
@@ -1418,7 +1527,7 @@ double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uin
   (void)hipEventRecord(t0, e->stream);
   for (int r = 0; r < reps; r++)
     if (search_device_impl(e, d_frames, d_refs, nframes, d_costs, nullptr, nullptr, nullptr, nullptr, e->stream,
-                           d_refs != nullptr && d_refs != d_frames) != 0) {
+                           d_refs != nullptr && d_refs != d_frames, device_status(e)) != 0) {
       (void)hipEventDestroy(t0);
       (void)hipEventDestroy(t1);
       return -1;
@@ -1429,7 +1538,7 @@ double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uin
   (void)hipEventElapsedTime(&ms, t0, t1);
   (void)hipEventDestroy(t0);
   (void)hipEventDestroy(t1);
-  if (check_status(e) != 0) return -1;
+  if (check_device_status(e) != 0) return -1;
   return ms / reps;
 }
 

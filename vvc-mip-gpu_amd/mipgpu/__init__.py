@@ -157,8 +157,12 @@ class _Ticket:
             return
         try:
             with eng._lock:
-                if getattr(eng, "_h", None):
-                    library().mip_wait(eng._h, ctypes.c_uint64(self.value))
+                if getattr(eng, "_h", None) and library().mip_wait(eng._h, ctypes.c_uint64(self.value)) != 0:
+                    # a finaliser cannot raise: a dropped call's error (e.g. the input contract,
+                    # reported per call by mip_wait) becomes a warning instead of vanishing
+                    import warnings
+                    warnings.warn("dropped search ticket %d failed: %s" % (self.value, library().mip_last_error().decode()),
+                                  RuntimeWarning, stacklevel=2)
         except Exception:
             pass
 
