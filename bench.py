@@ -63,6 +63,14 @@ VECTOR_OPS_PER_CTU = 99.6e6
 E2E_CALLS = 8  # host-buffer calls queued per end-to-end measurement
 
 
+def metric_name(width, height):
+    """BASELINE.json's metric for the 1080p workload; the same metric named for the frame size
+    otherwise (the config sweep's 4K / 8K lines are not 1080p frames)."""
+    if (width, height) == (1920, 1080):
+        return METRIC
+    return "%dx%d frames/sec, full MIP mode search over all CU sizes; 1/2/4/8 GPU" % (width, height)
+
+
 def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
@@ -121,6 +129,28 @@ def dist_max(value, world, device=None):
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def choose_backend(world, local_rank, ndev):
+    """(backend, device index) of a rank.  One rank per GPU: rank LOCAL_RANK on device
+    LOCAL_RANK, barriers and timing reductions over nccl (RCCL).  More ranks than GPUs (a
+    rehearsal of the N-GPU path on a smaller box) put rank r on device r % count and carry
+    them over gloo (RCCL needs a device per rank).  Frames stay sharded per rank either way."""
+    return ("nccl" if world <= ndev else "gloo"), local_rank % max(1, ndev)
+
+
+def init_ranks(world, local_rank, ndev):
+    """Process group of a multi-rank run (no-op for one rank); returns (backend, device index,
+    device of the collectives' tensors: None for gloo)."""
+    import torch
+    backend, dev_index = choose_backend(world, local_rank, ndev)
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    return backend, dev_index, (None if backend == "gloo" else torch.device("cuda", dev_index))
 
 
 def shard_seed(base_seed, rank):
@@ -254,8 +284,12 @@ def cpu_baseline(width, height, seed, budget_s=10.0):
         oracle_lib.search(frames[n % len(frames)], nthreads=threads)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "1080p frames/s" if (width, height) == (1920, 1080) else "frames/s",
-            "cores": threads, "kind": "port",
+    return {"value": round(n / dt, 4), "unit": "1080p frames/s" if (width, height) == (1920, 1080) else
+            "%dx%d frames/s" % (width, height), "cores": threads, "kind": "port",
+            "configs0": "BASELINE configs[0] names the reference's OpenCL kernels on the host CPU's OpenCL device; "
+                        "this image has no CPU OpenCL device (SURVEY.md 8c: the AMD ICD lists 0 CPU devices, no "
+                        "PoCL), so that run is not possible here -- this figure is the C port of the reference "
+                        "pipeline (oracle/mip_oracle.c), not the reference itself",
             "sample": "%d synthetic %dx%d frames (all CTUs, full search, same generator as the GPU run) through "
                       "the C oracle oracle/mip_oracle.c, OpenMP %d threads, %.1f s" % (n, width, height, threads, dt)}
 
@@ -416,19 +450,8 @@ def main():
     from mipgpu.synth import synth_frames_torch
 
     rank, local_rank, world = dist_env()
-    # One rank per GPU; more ranks than GPUs (a rehearsal of the N-GPU path on a smaller box)
-    # put rank r on device r % count and carry the barriers / timing reductions over gloo
-    # (RCCL needs a device per rank).  Frames stay sharded per rank either way.
     ndev = torch.cuda.device_count()
-    dev_index = local_rank % max(1, ndev)
-    backend = "nccl" if world <= ndev else "gloo"
-    if world > 1:
-        import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
-        else:
-            dist.init_process_group("gloo")
-    coll_dev = None if backend == "gloo" else torch.device("cuda", dev_index)
+    backend, dev_index, coll_dev = init_ranks(world, local_rank, ndev)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     W, H, B = args.width, args.height, args.frames_per_step
@@ -478,7 +501,7 @@ def main():
         build = build_id()
         pmc, pmc_src = load_pmc(W, H, B, build)
         res = {
-            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "metric": metric_name(W, H), "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16x2/int32",
             "data": "synthetic (seeded integer generator, mipgpu/synth.py, generated on the GPU)",

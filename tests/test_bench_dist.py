@@ -135,3 +135,33 @@ def test_valu_section_reports_both_issue_peaks():
     # without a PMC profile of this build the measured fields stay null
     v0 = bench.valu_section({}, 50.0, 1.0)
     assert v0["frac"] is None and "frac_of_dual_peak" not in v0
+
+
+@pytest.mark.parametrize("world,local_rank", [(8, 5), (8, 0), (2, 1)])
+def test_nccl_branch_with_one_device_per_rank(monkeypatch, world, local_rank):
+    """The driver's N-GPU run (one rank per GPU, device_count() == WORLD_SIZE): the rank's
+    process group is nccl (RCCL) bound to device LOCAL_RANK, and its collectives use that
+    device -- checked with the process-group constructor mocked (no GPU here)."""
+    calls = []
+    monkeypatch.setattr(dist, "init_process_group", lambda *a, **k: calls.append((a, k)))
+    backend, dev, coll = bench.init_ranks(world, local_rank, world)
+    assert (backend, dev) == ("nccl", local_rank)
+    assert coll == torch.device("cuda", local_rank)
+    assert calls == [(("nccl",), {"device_id": torch.device("cuda", local_rank)})]
+
+
+def test_gloo_branch_when_ranks_share_devices(monkeypatch):
+    """More ranks than GPUs (the one-GPU rehearsal of the 8-rank run): gloo, rank r on device
+    r % count, host-side collectives."""
+    calls = []
+    monkeypatch.setattr(dist, "init_process_group", lambda *a, **k: calls.append((a, k)))
+    assert bench.init_ranks(8, 5, 1) == ("gloo", 0, None)
+    assert calls == [(("gloo",), {})]
+    calls.clear()
+    assert bench.init_ranks(1, 0, 1)[:2] == ("nccl", 0) and calls == []  # one rank: no process group
+
+
+def test_metric_names_the_frame_size():
+    assert bench.metric_name(1920, 1080) == bench.METRIC
+    assert bench.metric_name(3840, 2160).startswith("3840x2160 frames/sec")
+    assert "1080p" not in bench.metric_name(7680, 4320)

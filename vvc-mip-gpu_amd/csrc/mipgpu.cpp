@@ -498,6 +498,10 @@ struct mip_engine {
   // k-1's download with frame k's search).
   static constexpr int kHostSlots = 4;
   int hp_slots = 0, hp_cap = 0, hp_frames = 0;  // hp_frames: frames of the engine buffers
+  // d_best_cost holds all ones outside the chunks in flight (decisions-only chunks need their
+  // split entries initialised); false after a failed call left a region in use, until the
+  // next call re-initialises it
+  bool best_cost_clean = true;
   hipEvent_t slot_up[kHostSlots] = {}, slot_comp[kHostSlots] = {}, slot_down[kHostSlots] = {};
   // Chunks run through the slots in one global sequence across host-API calls, so that
   // asynchronous calls (mip_search_frames_async) keep the pipeline full; call k completes
@@ -598,6 +602,14 @@ constexpr int kSmallLaunchItemsPerGroup = 32;
 // Per-item cost beyond its tasks (window staging, barriers, fills), in the task cost
 // model's units (pair_cost: VALU instructions per lane).
 constexpr double kItemOverhead = 600.0;
+
+// MIPGPU_DEC_INLINE=1 (A/B knob): decisions-only chunks of the host pipeline initialise and
+// unpack their split entries on the search stream (before round 5) instead of the download
+// stream.
+bool dec_inline() {
+  const char *e = getenv("MIPGPU_DEC_INLINE");
+  return e && *e == '1';
+}
 
 bool lpt_order_enabled() {
   const char *e = getenv("MIPGPU_ORDER");  // A/B knob: 0 = raster item order in small launches
@@ -889,9 +901,18 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail("hipStreamCreate failed"));
+  // The slot events order the engine's own streams on this device only (uploads -> search ->
+  // downloads; the kernels' dispatch packets carry the device-scope cache fences).
+  // MIPGPU_SLOT_EVENTS (A/B knob): "nofence" drops their system-scope fences
+  // (hipEventDisableSystemFence), "device" releases to device scope (hipEventReleaseToDevice).
+  unsigned slot_flags = hipEventDisableTiming;
+  if (const char *se = getenv("MIPGPU_SLOT_EVENTS")) {
+    if (!strcmp(se, "nofence")) slot_flags |= hipEventDisableSystemFence;
+    else if (!strcmp(se, "device")) slot_flags |= hipEventReleaseToDevice;
+  }
   for (int i = 0; i < mip_engine::kHostSlots; i++)
     for (hipEvent_t *ev : {&e->slot_up[i], &e->slot_comp[i], &e->slot_down[i]})
-      if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
+      if (hipEventCreateWithFlags(ev, slot_flags) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   for (hipEvent_t &ev : e->call_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   if (hipEventCreateWithFlags(&e->host_done, hipEventDisableTiming) != hipSuccess)
@@ -924,6 +945,10 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     e->resident_wide[alt] = mipgpu::search_resident_groups(alt != 0, true);
   }
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
+  // all ones: the decisions-only searches of the host pipeline find their split entries
+  // initialised (search_frames_chunks re-initialises every region a chunk used after its
+  // download)
+  if (hipMemset(e->d_best_cost, 0xff, ncu * o.best_k * 4) != hipSuccess) return cleanup(fail("hipMemset failed"));
   const CtuVariants cv = ctu_variants(width, height, o.filter);
   if (cv.pattern.size() > (size_t)mipgpu::kMaxCtuVariants)
     return cleanup(fail("too many CTU variants (%zu)", cv.pattern.size()));
@@ -1043,7 +1068,7 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
 static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
                               int32_t *d_best_cost, hipStream_t s, bool caller_refs, uint32_t *d_status,
-                              int ctu0 = 0, int nrange = -1) {
+                              int ctu0 = 0, int nrange = -1, mipgpu::SplitArgs *defer_split = nullptr) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
   // Decisions only (no cost table): the search writes each CU's decision into d_best /
   // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
@@ -1133,7 +1158,10 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   }
   const mipgpu::SplitArgs sa{work.d_split, work.d_split_begin, a.ctu_var, d_best, d_best_cost,
                              e->nctus, ctu0, nrange, work.max_split};
-  if (decisions_only) HIP_TRY(mipgpu::launch_dec_split(sa, nframes, true, s));
+  // defer_split (host pipeline): the split entries are already all ones and the caller
+  // unpacks them on its download stream (off the search stream's critical path)
+  if (decisions_only && defer_split) *defer_split = sa;
+  if (decisions_only && !defer_split) HIP_TRY(mipgpu::launch_dec_split(sa, nframes, true, s));
   const int slot = e->queue.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + mipgpu::kQueueWords * slot;
@@ -1158,7 +1186,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
     }
   }
   if (decisions_only) {
-    HIP_TRY(mipgpu::launch_dec_split(sa, nframes, false, s));
+    if (!defer_split) HIP_TRY(mipgpu::launch_dec_split(sa, nframes, false, s));
   } else if (d_best || d_best_cost) {
     mipgpu::BestArgs b{d_costs, d_best, d_best_cost, (int)total_cus, e->opts.best_k};
     HIP_TRY(mipgpu::launch_best_modes(b, s));
@@ -1248,6 +1276,10 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
     (void)e->stage.drain(e->host_calls);
     e->stage.abandon();
     (void)take_status(e, (int)((next - 1) % mip_engine::kCallRing));  // the failed call's chunks: no ticket
+    // a chunk may have used its d_best_cost region without the re-initialisation after its
+    // download: restore all ones (the streams are idle now)
+    const size_t nbest = (size_t)e->hp_frames * e->nctus * MIP_CUS_PER_CTU * e->opts.best_k * 4;
+    e->best_cost_clean = hipMemset(e->d_best_cost, 0xff, nbest) == hipSuccess;
     g_err = err;
     return rc;
   }
@@ -1322,8 +1354,12 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   };
   equal_chunks();
   if (!(pin_in && pin_cost && pin_sad && pin_satd && pin_bm && pin_bc)) {
-    const size_t most = std::max({(size_t)sb * fs * 2, (size_t)sb * cpf * 4, (size_t)sb * upf * 4});
-    HIP_TRY(e->stage.reserve(std::min<size_t>(most, mipgpu::HostStage::kMaxPiece)));
+    // pieces sized for a whole slot of the buffers this call moves (not for this call's
+    // chunk: a call into an idle pipeline is cut in two, and growing the ring later drains
+    // it and pins new memory)
+    const size_t per_frame = std::max({fs * 2, down_per_frame ? cpf * 4 : 0,
+                                       best_cost_out ? upf * 4 : (best_mode_out ? upf : 0)});
+    HIP_TRY(e->stage.reserve(std::min<size_t>((size_t)slot_cap * per_frame, mipgpu::HostStage::kMaxPiece)));
     // Pageable transfers are cut into ring pieces per buffer: a chunk's downloads must fit
     // the ring beside the next chunk's uploads (host_stage.h kMaxChunkPieces), else
     // enqueueing them waits on the host for the chunk's own search.  Counted per buffer
@@ -1395,17 +1431,27 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     int32_t *d_sad = sad_out ? e->d_sad + fo * cpf : nullptr, *d_satd = satd_out ? e->d_satd + fo * cpf : nullptr;
     uint8_t *d_best = best_mode_out ? e->d_best + fo * upf : nullptr;
     int32_t *d_best_cost = best_cost_out || decisions_only ? e->d_best_cost + fo * upf : nullptr;
+    // Decisions only: the split CUs' packed running minima live in d_best_cost, which holds
+    // all ones outside the chunks in flight (every chunk that used it re-initialises its
+    // region after its download, below), so the search stream runs the search kernel alone
+    // and the unpacking kernel runs on the download stream before the download -- the two
+    // small kernels and their launch gaps leave the search stream's critical path (one-frame
+    // calls: ~20 us of ~190 us per frame).
+    mipgpu::SplitArgs split{};
+    const bool defer = decisions_only && e->best_cost_clean && !dec_inline();
     if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
-                           refs_or_null != nullptr, call_status(e, call)) != 0)
+                           refs_or_null != nullptr, call_status(e, call), 0, -1, defer ? &split : nullptr) != 0)
       return -1;
     HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     if (!any_out) continue;
     HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));
+    if (defer) HIP_TRY(mipgpu::launch_dec_split(split, nb, false, down));
     if (costs_out) HIP_TRY(to_host(costs_out + f0 * cpf, d_costs, nb * cpf * 4, pin_cost));
     if (sad_out) HIP_TRY(to_host(sad_out + f0 * cpf, d_sad, nb * cpf * 4, pin_sad));
     if (satd_out) HIP_TRY(to_host(satd_out + f0 * cpf, d_satd, nb * cpf * 4, pin_satd));
     if (best_mode_out) HIP_TRY(to_host(best_mode_out + f0 * upf, d_best, nb * upf, pin_bm));
     if (best_cost_out) HIP_TRY(to_host(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, pin_bc));
+    if (d_best_cost) HIP_TRY(hipMemsetAsync(d_best_cost, 0xff, nb * upf * 4, down));
     HIP_TRY(hipEventRecord(e->slot_down[sl], down));
   }
   return 0;
