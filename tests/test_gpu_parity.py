@@ -713,3 +713,41 @@ def test_per_frame_calls_triple_buffered(gpu_available, w, filt, k):
             assert np.array_equal(o["cost"][0], oc), (i, kind)
         assert np.array_equal(o["best_mode"][0], bm), (i, kind)
         assert np.array_equal(o["best_cost"][0], bc), (i, kind)
+
+
+def test_per_frame_pipeline_stress_1080p(gpu_available):
+    """Ordering of the host pipeline's three streams under load at the bench size: 48
+    asynchronous one-frame 1080p calls in flight (three buffer slots reused 16 times each;
+    decisions only and full tables interleaved, page-locked buffers), frames drawn from a pool
+    of four -- every call's outputs equal a synchronous search of the same frame (a slot read
+    before its upload landed, or downloaded before its search finished, would show as a
+    mismatch)."""
+    from mipgpu import pinned_empty
+    W, H = 1920, 1080
+    pool = synth_frames(W, H, 4, 0x5F1, 0)
+    with MipEngine(W, H, max_batch=4) as ref_eng:
+        want = ref_eng.search(pool, best=True)
+    with MipEngine(W, H) as eng:
+        pf = pinned_empty(pool.shape, np.uint16)
+        pf[:] = pool
+        tickets, kinds = [], []
+        for i in range(48):
+            f = pf[i % 4:i % 4 + 1]
+            if i % 6 == 5:
+                out = {"cost": pinned_empty((1, eng.costs_per_frame), np.int32),
+                       "best_mode": pinned_empty((1, eng.cus_per_frame), np.uint8),
+                       "best_cost": pinned_empty((1, eng.cus_per_frame), np.int32)}
+                tickets.append(eng.search_async(f, best=True, out=out))
+                kinds.append("full")
+            else:
+                out = {"best_mode": pinned_empty((1, eng.cus_per_frame), np.uint8),
+                       "best_cost": pinned_empty((1, eng.cus_per_frame), np.int32)}
+                tickets.append(eng.search_async(f, costs=False, best=True, out=out))
+                kinds.append("dec")
+        outs = [eng.wait(t) for t in tickets]
+    for i, (kind, o) in enumerate(zip(kinds, outs)):
+        j = i % 4
+        assert np.array_equal(o["best_mode"][0], want["best_mode"][j]), (i, kind)
+        assert np.array_equal(o["best_cost"][0], want["best_cost"][j]), (i, kind)
+        if kind == "full":
+            assert np.array_equal(o["cost"][0], want["cost"][j]), i

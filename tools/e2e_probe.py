@@ -56,14 +56,21 @@ def run(case, W, H, calls, reps):
             o = {"cost": alloc((F, eng.costs_per_frame), np.int32)}
             kw = dict(out=o)
         eng.search(frames, **kw)
-        rates = []
+        rates, enq, wt = [], [], []
         for _ in range(reps):
             t0 = time.perf_counter()
-            eng.wait([eng.search_async(frames, **kw) for _ in range(calls)][-1])
-            rates.append(calls * F / (time.perf_counter() - t0))
+            tickets = [eng.search_async(frames, **kw) for _ in range(calls)]
+            t1 = time.perf_counter()
+            eng.wait(tickets[-1])
+            t2 = time.perf_counter()
+            rates.append(calls * F / (t2 - t0))
+            enq.append(1e3 * (t1 - t0))
+            wt.append(1e3 * (t2 - t1))
+            del tickets
     return {"case": case, "frames_per_call": F, "out": out, "host": host, "filter": flt, "kernel_idx": kidx,
             "max_batch": mb, "calls": calls, "fps": round(float(np.median(rates)), 1),
-            "fps_all": [round(r, 1) for r in rates]}
+            "fps_all": [round(r, 1) for r in rates], "enqueue_ms": [round(x, 3) for x in enq],
+            "wait_ms": [round(x, 3) for x in wt]}
 
 
 def main():

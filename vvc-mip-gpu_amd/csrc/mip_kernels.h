@@ -69,6 +69,10 @@ struct SearchArgs {
   // `dfill` lists.
   uint8_t *best_mode;     // optional
   int32_t *best_cost;
+  // optional: the split CUs' packed running argmins go here instead of best_cost (same CU
+  // indexing; all ones before the launch, reset to all ones by the unpacking launch_dec_split
+  // -- the host pipeline keeps it initialised across launches, so no init kernel runs)
+  uint32_t *split_acc;
   const uint16_t *dfill;  // undefined CUs of (v, q): CU indices inside the CTU,
   const int *dfill_begin; // [dfill_begin[4v+q], dfill_begin[4v+q+1])
   int32_t *sad;           // optional, same layout
@@ -180,7 +184,9 @@ hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 // Decisions only, CUs whose mode pairs are cut over several tasks (split CUs of the CTU's
 // variant: [split_begin[v], split_begin[v+1]) of `split`, at most max_split per variant):
 // init = true sets their best_cost entries to all ones (before the search); init = false
-// unpacks the packed argmin in place into best_mode / best_cost (after it).
+// unpacks the packed argmin in place into best_mode / best_cost (after it).  With `acc`
+// (SearchArgs::split_acc) the packed argmins are read from acc, which the unpacking resets
+// to all ones (init is then never needed).
 struct SplitArgs {
   const uint16_t *split;
   const int *split_begin;
@@ -188,6 +194,7 @@ struct SplitArgs {
   uint8_t *best_mode;
   int32_t *best_cost;
   int nctus, ctu0, nrange, max_split;
+  uint32_t *acc;
 };
 hipError_t launch_dec_split(const SplitArgs &a, int nframes, bool init, hipStream_t s);
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s);

@@ -1240,7 +1240,7 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_ti
       if (a.best_mode) a.best_mode[g] = (uint8_t)(best & 31);
       a.best_cost[g] = (int32_t)(best >> 5);
     } else {
-      atomicMin(reinterpret_cast<uint32_t *>(a.best_cost) + g, best);
+      atomicMin((a.split_acc ? a.split_acc : reinterpret_cast<uint32_t *>(a.best_cost)) + g, best);
     }
   }
 }
@@ -1870,9 +1870,16 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
   if (j >= a.split_begin[v + 1] - b) return;
   const size_t g = ((size_t)frame * a.nctus + ctu) * MIP_CUS_PER_CTU + a.split[b + j];
   if (INIT) {
-    a.best_cost[g] = -1;
+    if (a.acc) a.acc[g] = ~0u;
+    else a.best_cost[g] = -1;
   } else {
-    const uint32_t p = (uint32_t)a.best_cost[g];
+    uint32_t p;
+    if (a.acc) {
+      p = a.acc[g];
+      a.acc[g] = ~0u;  // initialised for the next launch
+    } else {
+      p = (uint32_t)a.best_cost[g];
+    }
     const bool ok = p != 0xffffffffu;
     if (a.best_mode) a.best_mode[g] = ok ? (uint8_t)(p & 31) : (uint8_t)0xff;
     a.best_cost[g] = ok ? (int32_t)(p >> 5) : kUnavailable;

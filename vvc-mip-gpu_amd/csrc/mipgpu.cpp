@@ -498,10 +498,10 @@ struct mip_engine {
   // k-1's download with frame k's search).
   static constexpr int kHostSlots = 4;
   int hp_slots = 0, hp_cap = 0, hp_frames = 0;  // hp_frames: frames of the engine buffers
-  // d_best_cost holds all ones outside the chunks in flight (decisions-only chunks need their
-  // split entries initialised); false after a failed call left a region in use, until the
-  // next call re-initialises it
-  bool best_cost_clean = true;
+  // Decisions-only chunks: the packed running argmins of the CUs whose mode pairs are cut
+  // over several tasks ([hp_frames][nCTUs][5380]); all ones outside the chunks in flight
+  // (the unpacking kernel resets the entries it reads), so no initialising kernel runs.
+  uint32_t *d_split_acc = nullptr;
   hipEvent_t slot_up[kHostSlots] = {}, slot_comp[kHostSlots] = {}, slot_down[kHostSlots] = {};
   // Chunks run through the slots in one global sequence across host-API calls, so that
   // asynchronous calls (mip_search_frames_async) keep the pipeline full; call k completes
@@ -509,9 +509,9 @@ struct mip_engine {
   uint64_t host_chunks = 0, host_calls = 0;
   static constexpr int kCallRing = 64;
   hipEvent_t call_done[kCallRing] = {};
-  // Last host-API search (stream `stream`): device-API searches that filter into the
-  // engine's reference scratch wait for it (the host pipeline uses the same buffer).
-  hipEvent_t host_done = nullptr;
+  // A host-API call was made: device-API searches that filter into the engine's reference
+  // scratch wait for the last call's completion, call_done[(host_calls - 1) % kCallRing]
+  // (the host pipeline uses the same buffer; no extra event on the search stream).
   bool host_pending = false;
   // mip_trace_times: per-slot timing events around the chunk's upload and filter launch,
   // the chunk (sequence number, frames) whose events are pending, and the per-frame times
@@ -568,17 +568,30 @@ struct mip_engine {
   static constexpr int kQueueSlots = 16;
   uint32_t *d_queue = nullptr;
   hipEvent_t queue_done[kQueueSlots] = {};
+  // Two rings: `queue` for device-API launches (any caller stream: reuse ordered by the
+  // slot's event) and `hp_queue` for the host pipeline, whose searches all run on the engine's
+  // own search stream `stream`: launches on one in-order stream never overlap, so its ring
+  // needs neither the event record nor the wait (two fewer queue packets per chunk on the
+  // search stream's critical path).  The pairs are distinct memory (hp_queue: slots
+  // kQueueSlots..2 kQueueSlots-1 of d_queue).
   struct QueueOps {
     mip_engine *e;
-    int wait(int slot, hipStream_t s) const { return hipStreamWaitEvent(s, e->queue_done[slot], 0) != hipSuccess; }
-    int record(int slot, hipStream_t s) const { return hipEventRecord(e->queue_done[slot], s) != hipSuccess; }
+    int base;           // first counter pair of the ring in d_queue
+    bool one_stream;    // every launch of the ring is on one stream: no events needed
+    int wait(int slot, hipStream_t s) const {
+      return one_stream ? 0 : hipStreamWaitEvent(s, e->queue_done[slot], 0) != hipSuccess;
+    }
+    int record(int slot, hipStream_t s) const {
+      return one_stream ? 0 : hipEventRecord(e->queue_done[slot], s) != hipSuccess;
+    }
     int clear(int slot, hipStream_t s) const {
-      return hipMemsetAsync(e->d_queue + mipgpu::kQueueWords * slot, 0, mipgpu::kQueueWords * sizeof(uint32_t), s) !=
-             hipSuccess;
+      return hipMemsetAsync(e->d_queue + mipgpu::kQueueWords * (base + slot), 0, mipgpu::kQueueWords * sizeof(uint32_t),
+                            s) != hipSuccess;
     }
     int sync(hipStream_t s) const { return hipStreamSynchronize(s) != hipSuccess; }
   };
-  QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this}};
+  QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this, 0, false}};
+  QueueRing<QueueOps, kQueueSlots> hp_queue{QueueOps{this, kQueueSlots, true}};
   // Input contract (10-bit samples): status words the search kernel sets when it stages a
   // sample above 1023 (SearchArgs::status), in page-locked host memory mapped into the
   // device.  One set of kStatusWords per host-API call (call c: set (c - 1) % kCallRing) and
@@ -816,7 +829,8 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream3) (void)hipStreamSynchronize(e->stream3);
   e->stage.abandon();
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
-                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_tables})
+                  (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_split_acc,
+                  (void *)e->d_tables})
     if (p) (void)hipFree(p);
   for (int m = 0; m < kMaps; m++) {
     if (e->d_ctu_var[m]) (void)hipFree(e->d_ctu_var[m]);
@@ -832,7 +846,6 @@ int mip_engine_destroy(mip_engine *e) {
       if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : e->call_done)
     if (ev) (void)hipEventDestroy(ev);
-  if (e->host_done) (void)hipEventDestroy(e->host_done);
   for (auto &evs : e->tr_ev)
     for (hipEvent_t ev : evs)
       if (ev) (void)hipEventDestroy(ev);
@@ -915,8 +928,6 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
       if (hipEventCreateWithFlags(ev, slot_flags) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   for (hipEvent_t &ev : e->call_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
-  if (hipEventCreateWithFlags(&e->host_done, hipEventDisableTiming) != hipSuccess)
-    return cleanup(fail("hipEventCreate failed"));
   ALLOC(e->d_frames, fs * nb * 2);
   if (o.filter != MIP_FILTER_NONE) ALLOC(e->d_refs, fs * nb * 2);
   ALLOC(e->d_costs, ncost * 4);
@@ -925,8 +936,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     ALLOC(e->d_satd, ncost * 4);
   }
   ALLOC(e->d_best, ncu * o.best_k);
-  ALLOC(e->d_queue, mipgpu::kQueueWords * mip_engine::kQueueSlots * sizeof(uint32_t));
-  if (hipMemset(e->d_queue, 0, mipgpu::kQueueWords * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
+  ALLOC(e->d_queue, mipgpu::kQueueWords * 2 * mip_engine::kQueueSlots * sizeof(uint32_t));
+  if (hipMemset(e->d_queue, 0, mipgpu::kQueueWords * 2 * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail("hipMemset failed"));
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
@@ -945,10 +956,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     e->resident_wide[alt] = mipgpu::search_resident_groups(alt != 0, true);
   }
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
-  // all ones: the decisions-only searches of the host pipeline find their split entries
-  // initialised (search_frames_chunks re-initialises every region a chunk used after its
-  // download)
-  if (hipMemset(e->d_best_cost, 0xff, ncu * o.best_k * 4) != hipSuccess) return cleanup(fail("hipMemset failed"));
+  ALLOC(e->d_split_acc, ncu * 4);
+  if (hipMemset(e->d_split_acc, 0xff, ncu * 4) != hipSuccess) return cleanup(fail("hipMemset failed"));
   const CtuVariants cv = ctu_variants(width, height, o.filter);
   if (cv.pattern.size() > (size_t)mipgpu::kMaxCtuVariants)
     return cleanup(fail("too many CTU variants (%zu)", cv.pattern.size()));
@@ -1068,7 +1077,8 @@ int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int heig
 static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
                               int32_t *d_best_cost, hipStream_t s, bool caller_refs, uint32_t *d_status,
-                              int ctu0 = 0, int nrange = -1, mipgpu::SplitArgs *defer_split = nullptr) {
+                              int ctu0 = 0, int nrange = -1, uint32_t *split_acc = nullptr,
+                              mipgpu::SplitArgs *defer_split = nullptr) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
   // Decisions only (no cost table): the search writes each CU's decision into d_best /
   // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
@@ -1089,7 +1099,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   if (engine_refs) {
     if (nframes > e->opts.max_batch) return fail("nframes %d > max_batch %d", nframes, e->opts.max_batch);
     if (e->refs_pending) HIP_TRY(hipStreamWaitEvent(s, e->refs_done, 0));  // last reader of d_refs
-    if (e->host_pending) HIP_TRY(hipStreamWaitEvent(s, e->host_done, 0));  // host calls in flight
+    if (e->host_pending)  // host calls in flight (calls complete in order: the last one)
+      HIP_TRY(hipStreamWaitEvent(s, e->call_done[(e->host_calls - 1) % mip_engine::kCallRing], 0));
     if (mip_filter_device(d_frames, e->d_refs, e->width, e->height, nframes, e->opts.filter,
                           e->opts.kernel_idx, s) != 0)
       return -1;
@@ -1156,21 +1167,27 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
       }
     }
   }
+  // split_acc + defer_split (host pipeline): the split CUs meet in split_acc, which holds all
+  // ones outside the launches in flight, and the caller unpacks (and re-initialises) it on
+  // its download stream -- no kernel but the search on the search stream
+  if (decisions_only && split_acc && defer_split) a.split_acc = split_acc;
+  else defer_split = nullptr;
   const mipgpu::SplitArgs sa{work.d_split, work.d_split_begin, a.ctu_var, d_best, d_best_cost,
-                             e->nctus, ctu0, nrange, work.max_split};
-  // defer_split (host pipeline): the split entries are already all ones and the caller
-  // unpacks them on its download stream (off the search stream's critical path)
-  if (decisions_only && defer_split) *defer_split = sa;
+                             e->nctus, ctu0, nrange, work.max_split, a.split_acc};
+  if (defer_split) *defer_split = sa;
   if (decisions_only && !defer_split) HIP_TRY(mipgpu::launch_dec_split(sa, nframes, true, s));
-  const int slot = e->queue.acquire(s);
+  // the host pipeline's launches (all on the engine's search stream) use their own ring
+  auto &ring = s == e->stream ? e->hp_queue : e->queue;
+  const int qbase = s == e->stream ? mip_engine::kQueueSlots : 0;
+  const int slot = ring.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
-  a.queue = e->d_queue + mipgpu::kQueueWords * slot;
+  a.queue = e->d_queue + mipgpu::kQueueWords * (qbase + slot);
   const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, s);
   if (le != hipSuccess) {
-    e->queue.failed(slot);  // the pair is cleared before its next use
+    ring.failed(slot);  // the pair is cleared before its next use
     return fail("search launch failed: %s", hipGetErrorString(le));
   }
-  if (e->queue.launched(slot, s) != 0) return fail("hipEventRecord failed");
+  if (ring.launched(slot, s) != 0) return fail("hipEventRecord failed");
   if (alt && e->nfixup[map]) HIP_TRY(mipgpu::launch_fixup(a, e->d_fixup[map], e->nfixup[map], nframes, s));
   if (engine_refs) {
     HIP_TRY(hipEventRecord(e->refs_done, s));
@@ -1261,12 +1278,8 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
   }
   const int rc = search_frames_chunks(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out,
                                       sad_out, satd_out, next);
-  // Also after a failure part-way through the chunks: the chunks already queued on the
-  // upload / search streams are covered by host_done (later device-API searches that filter
-  // into the engine's reference scratch wait for it) and by this call's completion event.
-  const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
-  if (hipEventRecord(e->host_done, e->stream) != hipSuccess) return rc ? rc : fail("hipEventRecord failed");
-  e->host_pending = true;
+  // After a failure part-way through the chunks, the chunks already queued are waited for
+  // here (no ticket covers them).
   if (rc != 0) {
     const std::string err = g_err;
     (void)hipStreamSynchronize(e->stream2);
@@ -1276,18 +1289,17 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
     (void)e->stage.drain(e->host_calls);
     e->stage.abandon();
     (void)take_status(e, (int)((next - 1) % mip_engine::kCallRing));  // the failed call's chunks: no ticket
-    // a chunk may have used its d_best_cost region without the re-initialisation after its
-    // download: restore all ones (the streams are idle now)
-    const size_t nbest = (size_t)e->hp_frames * e->nctus * MIP_CUS_PER_CTU * e->opts.best_k * 4;
-    e->best_cost_clean = hipMemset(e->d_best_cost, 0xff, nbest) == hipSuccess;
+    // a decisions-only chunk may have been searched without its unpacking (which resets its
+    // split_acc entries): restore all ones (the streams are idle now)
+    (void)hipMemset(e->d_split_acc, 0xff, (size_t)e->hp_frames * e->nctus * MIP_CUS_PER_CTU * 4);
     g_err = err;
     return rc;
   }
-  // completion on the download stream, after this call's search and every earlier call's
-  // downloads: calls complete in order
-  if (!any_out) HIP_TRY(hipStreamWaitEvent(e->stream3, e->host_done, 0));
+  // completion on the download stream (every chunk ends there, after its search and
+  // downloads, outputs or not): calls complete in order
   const uint64_t call = ++e->host_calls;
   HIP_TRY(hipEventRecord(e->call_done[(call - 1) % mip_engine::kCallRing], e->stream3));
+  e->host_pending = true;
   *ticket = call;
   return 0;
 }
@@ -1341,7 +1353,6 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     sb = std::max(1, std::min<int>(sb, (int)(cap / down_per_frame)));
   }
   const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
-  const bool any_out = costs_out || sad_out || satd_out || best_mode_out || best_cost_out;
   const bool pin_in = mipgpu::HostStage::pinned(frames) && (!refs_or_null || mipgpu::HostStage::pinned(refs_or_null));
   const bool pin_cost = !costs_out || mipgpu::HostStage::pinned(costs_out);
   const bool pin_sad = !sad_out || mipgpu::HostStage::pinned(sad_out);
@@ -1392,7 +1403,11 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     const bool reuse = k >= (uint64_t)nslots;  // the slot served chunk k - nslots (this or an earlier call)
     const size_t fo = (size_t)sl * slot_cap;  // first engine frame of this chunk's slot
     uint16_t *d_frames = e->d_frames + fo * fs;
-    if (reuse) HIP_TRY(hipStreamWaitEvent(up, e->slot_comp[sl], 0));
+    // the slot's previous chunk is over once its downloads are (they wait for its search):
+    // then its frames / refs may be overwritten here, and -- through this upload -- its
+    // outputs by this chunk's search, which waits for nothing else (one cross-stream wait
+    // on the search stream per chunk)
+    if (reuse) HIP_TRY(hipStreamWaitEvent(up, e->slot_down[sl], 0));
     if (e->trace) {
       if (drain_trace(e, sl) != 0) return -1;
       HIP_TRY(hipEventRecord(e->tr_ev[sl][0], up));
@@ -1418,7 +1433,6 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     }
     HIP_TRY(hipEventRecord(e->slot_up[sl], up));
     HIP_TRY(hipStreamWaitEvent(comp, e->slot_up[sl], 0));
-    if (reuse) HIP_TRY(hipStreamWaitEvent(comp, e->slot_down[sl], 0));
     if (e->trace) {
       e->tr_frames[sl] = nb;
       e->tr_filter[sl] = filt;
@@ -1431,27 +1445,26 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     int32_t *d_sad = sad_out ? e->d_sad + fo * cpf : nullptr, *d_satd = satd_out ? e->d_satd + fo * cpf : nullptr;
     uint8_t *d_best = best_mode_out ? e->d_best + fo * upf : nullptr;
     int32_t *d_best_cost = best_cost_out || decisions_only ? e->d_best_cost + fo * upf : nullptr;
-    // Decisions only: the split CUs' packed running minima live in d_best_cost, which holds
-    // all ones outside the chunks in flight (every chunk that used it re-initialises its
-    // region after its download, below), so the search stream runs the search kernel alone
-    // and the unpacking kernel runs on the download stream before the download -- the two
-    // small kernels and their launch gaps leave the search stream's critical path (one-frame
-    // calls: ~20 us of ~190 us per frame).
+    // Decisions only: the split CUs' packed running minima live in d_split_acc, which holds
+    // all ones outside the chunks in flight (the unpacking resets what it reads), so the
+    // search stream runs the search kernel alone and the unpacking runs on the download
+    // stream before the download -- the initialising and unpacking kernels and their launch
+    // gaps leave the search stream's critical path (one-frame calls: ~20 us of ~190 us).
     mipgpu::SplitArgs split{};
-    const bool defer = decisions_only && e->best_cost_clean && !dec_inline();
+    const bool defer = decisions_only && !dec_inline();
     if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
-                           refs_or_null != nullptr, call_status(e, call), 0, -1, defer ? &split : nullptr) != 0)
+                           refs_or_null != nullptr, call_status(e, call), 0, -1,
+                           defer ? e->d_split_acc + fo * e->nctus * MIP_CUS_PER_CTU : nullptr,
+                           defer ? &split : nullptr) != 0)
       return -1;
     HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
-    if (!any_out) continue;
-    HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));
+    HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));  // (also without outputs: slot_down ends the chunk)
     if (defer) HIP_TRY(mipgpu::launch_dec_split(split, nb, false, down));
     if (costs_out) HIP_TRY(to_host(costs_out + f0 * cpf, d_costs, nb * cpf * 4, pin_cost));
     if (sad_out) HIP_TRY(to_host(sad_out + f0 * cpf, d_sad, nb * cpf * 4, pin_sad));
     if (satd_out) HIP_TRY(to_host(satd_out + f0 * cpf, d_satd, nb * cpf * 4, pin_satd));
     if (best_mode_out) HIP_TRY(to_host(best_mode_out + f0 * upf, d_best, nb * upf, pin_bm));
     if (best_cost_out) HIP_TRY(to_host(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, pin_bc));
-    if (d_best_cost) HIP_TRY(hipMemsetAsync(d_best_cost, 0xff, nb * upf * 4, down));
     HIP_TRY(hipEventRecord(e->slot_down[sl], down));
   }
   return 0;
