@@ -111,10 +111,15 @@ int mip_unavailable_cus(int width, int height, int filter, uint8_t *cu_out);
 int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int filter,
                       int kernel_idx, uint16_t *out);
 
-/* Full MIP search of `nframes` host frames: H2D, [filter], search, D2H, in chunks of
- * max_batch/4 (max_batch >= 16) or max_batch/2 frames through the engine's three streams
- * (uploads, search, downloads), so that one chunk's upload, the previous chunk's search and
- * the one before's download run at the same time.
+/* Full MIP search of `nframes` host frames: H2D, [filter], search, D2H, in chunks through
+ * the engine's three streams (uploads, search, downloads) and buffer slots -- 4 slots of
+ * max_batch/4 frames (max_batch >= 16), else 3 slots of max_batch frames (the engine's
+ * buffers hold 3 x max_batch frames then) -- so that one chunk's upload, the previous
+ * chunk's search and the one before's download run at the same time, also across calls:
+ * an engine searching one frame per call (max_batch 1, the reference's per-frame loop with
+ * BUFFER_SLOTS 2, main.cpp:886-898, main_aux_functions.h:5, 617) overlaps frame k+1's
+ * upload and frame k-1's download with frame k's search when the calls are queued with
+ * mip_search_frames_async.  A call into an idle pipeline is cut into two chunks.
  * Replaces the per-frame loop main.cpp:678-1241 + readMemobjsIntoArray_Distortion.
  * refs_or_null: caller-provided reference-sample frames (alternative samples computed
  * elsewhere); NULL = originals, or the engine's filter when opts.filter != NONE.
@@ -125,7 +130,7 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
  * sad_out / satd_out: optional (need opts.want_sad_satd).  Synchronous.
  * Host buffers: page-locked memory (mip_host_alloc, hipHostRegister) is transferred by DMA
  * directly; pageable memory (malloc, the reference's return_minSadHad, main.cpp:656-668)
- * goes through the engine's page-locked bounce ring (8 pieces of up to 64 MB, parallel host
+ * goes through the engine's page-locked bounce ring (16 pieces of up to 64 MB, parallel host
  * copies), allocated at its first use. */
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
                       int nframes, int32_t *costs_out, uint8_t *best_mode_out,
@@ -143,7 +148,9 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
 
 /* Block until the call with this ticket (and every earlier one) has completed: its outputs
  * are in host memory.  Pageable output buffers are written (copied out of the bounce ring)
- * by this call -- an asynchronous call with pageable outputs must be waited for. */
+ * by this call -- an asynchronous call with pageable outputs must be waited for.  Fails
+ * if THIS call's search staged a sample above 1023 (input contract; every call has its own
+ * status, so an earlier or later call's violation is reported by that call's own wait). */
 int mip_wait(mip_engine *e, uint64_t ticket);
 
 /* Device-resident variant (inputs already in HBM; all pointers are device pointers,

@@ -179,7 +179,10 @@ constexpr int kSearchWaves = 8, kWideWaves = 16;
 // Workgroups of the search kernel resident on the current device at once (persistent grid
 // size); computed once per engine (mip_engine_create), 0 on error.
 int search_resident_groups(bool alt_refs, bool wide);
-hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s);
+// done: optional event recorded by the kernel's own dispatch (hipExtLaunchKernel's stop
+// event) instead of a separate marker packet behind it.
+hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s,
+                         hipEvent_t done = nullptr);
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 // Decisions only, CUs whose mode pairs are cut over several tasks (split CUs of the CTU's
 // variant: [split_begin[v], split_begin[v+1]) of `split`, at most max_split per variant):

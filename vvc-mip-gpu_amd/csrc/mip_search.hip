@@ -34,6 +34,8 @@
 #include <type_traits>
 #include <utility>
 
+#include <hip/hip_ext.h>
+
 #include "mip_kernels.h"
 #include "mip_tables.h"
 
@@ -101,6 +103,11 @@ constexpr int kEntryBytes = 16;                         // 8 f16 MFMA inputs per
 constexpr int kCuTableBytes = 64 * kEntryBytes;
 constexpr int kScratchWords = 1280;                     // [slot][position] packed mode pairs
 constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
+#ifndef MIP_WAVE_STRIDE
+#define MIP_WAVE_STRIDE kWaveBytes  // LDS bytes between waves' private areas; smaller values
+                                    // overlap them (wrong results: occupancy-bound experiments)
+#endif
+constexpr int kWaveStride = MIP_WAVE_STRIDE;
 constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 16;    // > every uniform B offset + 8 B
 constexpr int kUnavailable = 0x7fffffff;
 
@@ -1635,7 +1642,7 @@ __device__ __forceinline__ void pair_loop(const SearchArgs &a, uint16_t *org_buf
       const int k = t < 2 * m ? t >> 1 : t - m;
       const uint64_t c0 = clk0 ? __builtin_readcyclecounter() : 0;
       const WaveTask task = a.tasks[(second ? tb1 : tb0) + k];
-      const Ctx x{&a, second ? org1 : org0, second ? org1 : org0, w, zero, waves + wave * kWaveBytes,
+      const Ctx x{&a, second ? org1 : org0, second ? org1 : org0, w, zero, waves + wave * kWaveStride,
                   second ? p1.ctu : p0.ctu, second ? p1.frame : p0.frame, second ? p1.fx0 : p0.fx0,
                   second ? p1.fy0 : p0.fy0};
       const RefTile<false> rt{x.ref};
@@ -1653,8 +1660,11 @@ __device__ __forceinline__ void pair_loop(const SearchArgs &a, uint16_t *org_buf
 
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
 // NW: waves per workgroup (kSearchWaves; kWideWaves: one workgroup per CU, small launches)
+#ifndef MIP_WAVES_PER_EU
+#define MIP_WAVES_PER_EU 4  // HIP-Clang: the second launch bound is the minimum waves per SIMD
+#endif
 template <bool ALT, bool DEC, bool PF_, int NW>
-__global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
+__global__ __launch_bounds__(64 * NW, MIP_WAVES_PER_EU) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = PF_ && !ALT && NW == kSearchWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles windows
@@ -1662,7 +1672,7 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
   uint8_t *w = smem + (kOrgTiles<ALT, PF, NW> * kTileElems + (ALT ? kLatElems : 0)) * 2;
   uint8_t *zero = w + kTableBytes;
   uint8_t *waves = zero + kZeroBytes;
-  uint32_t *counters = reinterpret_cast<uint32_t *>(waves + NW * kWaveBytes);
+  uint32_t *counters = reinterpret_cast<uint32_t *>(waves + NW * kWaveStride);
 
   for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(w)[i] = a.tables[i];
@@ -1712,7 +1722,7 @@ __global__ __launch_bounds__(64 * NW, 4) void mip_search_kernel(SearchArgs a) {
         __syncthreads();
       }
 
-      const Ctx x{&a, org, ref, w, zero, waves + wave * kWaveBytes, ctu, frame, fx0, fy0};
+      const Ctx x{&a, org, ref, w, zero, waves + wave * kWaveStride, ctu, frame, fx0, fy0};
       const RefTile<ALT> rt{ref};
       // Waves take the item's tasks (longest first) from an LDS counter, so early
       // finishers pick up the slack of waves the SIMD arbiter serves later.
@@ -1891,7 +1901,7 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
 size_t search_lds_bytes(bool alt, bool pf, int waves) {
   const bool two = (pf || waves == kWideWaves) && !alt;  // kOrgTiles
   return (size_t)((two ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
-         (size_t)waves * kWaveBytes + kCounterWords * 4;
+         (size_t)waves * kWaveStride + kCounterWords * 4;
 }
 
 template <bool ALT, bool DEC, bool PF, int NW>
@@ -1918,7 +1928,8 @@ int search_resident_groups(bool alt, bool wide) {
   return per_cu >= 1 ? cus * per_cu : 0;
 }
 
-hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s) {
+hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s,
+                         hipEvent_t done) {
   if (args.slices < 1 || !args.queue || !args.status || resident < 1) return hipErrorInvalidValue;
   SearchArgs a = args;
   if (a.ctu0 < 0 || a.nrange < 1 || a.ctu0 + a.nrange > a.nctus) return hipErrorInvalidValue;
@@ -1943,27 +1954,31 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const size_t lds = search_lds_bytes(alt_refs, pf, wide ? kWideWaves : kSearchWaves);
   const dim3 grid(groups);
   constexpr int S = kSearchWaves, L = kWideWaves;
+  auto go = [&](auto kern, const dim3 &block) {  // with `done`: the dispatch itself records it (no marker packet)
+    if (done) hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)lds, s, nullptr, done, 0u, a);
+    else hipLaunchKernelGGL(kern, grid, block, lds, s, a);
+  };
   if (wide) {
     const dim3 block(64 * L);
     if (alt_refs) {
-      if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true, false, L>), grid, block, lds, s, a);
-      else hipLaunchKernelGGL((mip_search_kernel<true, false, false, L>), grid, block, lds, s, a);
+      if (dec) go(mip_search_kernel<true, true, false, L>, block);
+      else go(mip_search_kernel<true, false, false, L>, block);
     } else {
-      if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, false, L>), grid, block, lds, s, a);
-      else hipLaunchKernelGGL((mip_search_kernel<false, false, false, L>), grid, block, lds, s, a);
+      if (dec) go(mip_search_kernel<false, true, false, L>, block);
+      else go(mip_search_kernel<false, false, false, L>, block);
     }
     return hipGetLastError();
   }
   const dim3 block(64 * S);
   if (alt_refs) {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<true, true, false, S>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<true, false, false, S>), grid, block, lds, s, a);
+    if (dec) go(mip_search_kernel<true, true, false, S>, block);
+    else go(mip_search_kernel<true, false, false, S>, block);
   } else if (pf) {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, true, S>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<false, false, true, S>), grid, block, lds, s, a);
+    if (dec) go(mip_search_kernel<false, true, true, S>, block);
+    else go(mip_search_kernel<false, false, true, S>, block);
   } else {
-    if (dec) hipLaunchKernelGGL((mip_search_kernel<false, true, false, S>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((mip_search_kernel<false, false, false, S>), grid, block, lds, s, a);
+    if (dec) go(mip_search_kernel<false, true, false, S>, block);
+    else go(mip_search_kernel<false, false, false, S>, block);
   }
   return hipGetLastError();
 }

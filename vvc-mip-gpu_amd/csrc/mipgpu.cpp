@@ -624,6 +624,13 @@ bool dec_inline() {
   return e && *e == '1';
 }
 
+// MIPGPU_EXT_DONE=0 (A/B knob): record the host pipeline's per-chunk completion event as a
+// separate marker instead of on the search kernel's dispatch.
+bool ext_done_enabled() {
+  const char *e = getenv("MIPGPU_EXT_DONE");
+  return !(e && *e == '0');
+}
+
 bool lpt_order_enabled() {
   const char *e = getenv("MIPGPU_ORDER");  // A/B knob: 0 = raster item order in small launches
   return !(e && *e == '0');
@@ -1078,7 +1085,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
                               int32_t *d_best_cost, hipStream_t s, bool caller_refs, uint32_t *d_status,
                               int ctu0 = 0, int nrange = -1, uint32_t *split_acc = nullptr,
-                              mipgpu::SplitArgs *defer_split = nullptr) {
+                              mipgpu::SplitArgs *defer_split = nullptr, hipEvent_t *done = nullptr) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
   // Decisions only (no cost table): the search writes each CU's decision into d_best /
   // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
@@ -1182,7 +1189,14 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const int slot = ring.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + mipgpu::kQueueWords * (qbase + slot);
-  const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, s);
+  // done (host pipeline): the chunk's completion event, recorded by the search kernel's own
+  // dispatch when nothing follows it on s (saves a marker packet between two chunks'
+  // searches); *done = nullptr tells the caller it was recorded
+  const bool last = !(alt && e->nfixup[map]) && !engine_refs && !timing &&
+                    (decisions_only ? defer_split != nullptr : !(d_best || d_best_cost)) && ext_done_enabled();
+  hipEvent_t stop = done && last ? *done : nullptr;
+  const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, s, stop);
+  if (le == hipSuccess && stop) *done = nullptr;
   if (le != hipSuccess) {
     ring.failed(slot);  // the pair is cleared before its next use
     return fail("search launch failed: %s", hipGetErrorString(le));
@@ -1452,12 +1466,13 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     // gaps leave the search stream's critical path (one-frame calls: ~20 us of ~190 us).
     mipgpu::SplitArgs split{};
     const bool defer = decisions_only && !dec_inline();
+    hipEvent_t comp_done = e->slot_comp[sl];  // (nullptr after the call: the search recorded it)
     if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
                            refs_or_null != nullptr, call_status(e, call), 0, -1,
                            defer ? e->d_split_acc + fo * e->nctus * MIP_CUS_PER_CTU : nullptr,
-                           defer ? &split : nullptr) != 0)
+                           defer ? &split : nullptr, &comp_done) != 0)
       return -1;
-    HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
+    if (comp_done) HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));  // (also without outputs: slot_down ends the chunk)
     if (defer) HIP_TRY(mipgpu::launch_dec_split(split, nb, false, down));
     if (costs_out) HIP_TRY(to_host(costs_out + f0 * cpf, d_costs, nb * cpf * 4, pin_cost));
