@@ -41,7 +41,31 @@ def parse(case):
     return f, out, host, flt, kidx, mb or f
 
 
-def run(case, W, H, calls, reps):
+def torch_steps(step, W, H):
+    """Use the GPU through torch as bench.py does, up to `step`: init | alloc | stream | d2h |
+    d2h_pinned (each includes the ones before it, d2h_pinned excepted d2h)."""
+    import torch
+    steps = ["init", "alloc", "stream", "d2h", "d2h_pinned"]
+    upto = steps.index(step)
+    torch.cuda.set_device(0)
+    torch.cuda.init()
+    x = None
+    if upto >= 1:
+        x = torch.randint(0, 1024, (8, H, W), dtype=torch.int16, device="cuda")
+    if upto >= 2:
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            x = x * 2
+        torch.cuda.synchronize()
+    if upto == 3:
+        _ = x[:2].cpu()
+    if upto == 4:
+        h = torch.empty(x[:2].shape, dtype=x.dtype, pin_memory=True)
+        h.copy_(x[:2], non_blocking=True)
+    torch.cuda.synchronize()
+
+
+def run(case, W, H, calls, reps, torch_after=None, device_first=0):
     F, out, host, flt, kidx, mb = parse(case)
     src = synth_frames(W, H, min(F, 4), 0x1080, 0)
     alloc = (lambda shape, dt: pinned_empty(shape, dt)) if host == "pinned" else (lambda shape, dt: np.zeros(shape, dt))
@@ -49,6 +73,15 @@ def run(case, W, H, calls, reps):
     for i in range(F):
         frames[i] = src[i % src.shape[0]]
     with MipEngine(W, H, max_batch=mb, filter=flt, kernel_idx=kidx) as eng:
+        if torch_after:  # torch's streams created after the engine's
+            torch_steps(torch_after, W, H)
+        if device_first:  # device-API searches of the same engine first (bench.py's timed steps)
+            import torch
+            d = torch.from_numpy(np.ascontiguousarray(frames).view(np.int16)).cuda()
+            st = torch.cuda.Stream()
+            for _ in range(device_first):
+                eng.search_device(d, stream=st)
+            torch.cuda.synchronize()
         if out == "dec":
             o = {"best_mode": alloc((F, eng.cus_per_frame), np.uint8), "best_cost": alloc((F, eng.cus_per_frame), np.int32)}
             kw = dict(costs=False, best=True, out=o)
@@ -80,9 +113,14 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--torch", default="", help="torch_steps(STEP) before the engines are created")
+    ap.add_argument("--torch-after", default="", help="torch_steps(STEP) after each engine is created")
+    ap.add_argument("--device-first", type=int, default=0, help="device-API searches of the engine first")
     a = ap.parse_args()
+    if a.torch:
+        torch_steps(a.torch, a.width, a.height)
     for c in a.cases:
-        print(json.dumps(run(c, a.width, a.height, a.calls, a.reps)), flush=True)
+        print(json.dumps(run(c, a.width, a.height, a.calls, a.reps, a.torch_after, a.device_first)), flush=True)
         time.sleep(0.2)
 
 

@@ -8,6 +8,16 @@ cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out}/multirank
 mkdir -p "$OUT"
 ARGS="--frames-per-step 128 --steps 10 --warmup 2 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter --no-end-to-end"
+# the driver's 8-GPU launch shape, rehearsed with 8 ranks on this box's one device (round 5:
+# launcher, rendezvous, `ranks`, max over 8 ranks; 32 frames per rank keep 8 engines in HBM)
+ARGS8="--frames-per-step 32 --steps 10 --warmup 2 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter --no-end-to-end"
+echo "== bench --gpus 8 (own ranks, 8 ranks sharing device 0) $(date +%T)"
+timeout -k 10 400 python bench.py --gpus 8 $ARGS8 > "$OUT/bench_gpus8.json" 2> "$OUT/bench_gpus8.err" || { tail -20 "$OUT/bench_gpus8.err"; exit 1; }
+cat "$OUT/bench_gpus8.json"
+echo "== torch.distributed.run --nproc-per-node 8 $(date +%T)"
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 8 $ARGS8 > "$OUT/bench_torchrun8.json" 2> "$OUT/bench_torchrun8.err" || { tail -20 "$OUT/bench_torchrun8.err"; exit 1; }
+cat "$OUT/bench_torchrun8.json"
 echo "== bench --gpus 2 (own ranks) $(date +%T)"
 timeout -k 10 300 python bench.py --gpus 2 $ARGS > "$OUT/bench_gpus2.json" 2> "$OUT/bench_gpus2.err" || { tail -20 "$OUT/bench_gpus2.err"; exit 1; }
 cat "$OUT/bench_gpus2.json"

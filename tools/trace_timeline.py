@@ -17,7 +17,7 @@ def short(name):
     n = name.split("(")[0]
     for key in ("mip_search_kernel", "dec_split_kernel", "best_mode_kernel", "filter_kernel", "fixup_kernel"):
         if key in name:
-            return key.replace("_kernel", "") + ("<dec>" if key == "mip_search_kernel" and "true, false" in name else "")
+            return key.replace("_kernel", "")
     return n[-32:]
 
 
@@ -28,10 +28,11 @@ def load(d):
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                        r.get("Stream_Id") or r.get("Queue_Id", "?")))
     for path in glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=True):
-        for r in csv.DictReader(open(path)):
+        rd = csv.DictReader(open(path))
+        for r in rd:
             dirn = r.get("Direction", "")
             kind = "H2D" if "HOST_TO_DEVICE" in dirn else ("D2H" if "DEVICE_TO_HOST" in dirn else dirn[-12:] or "copy")
-            nbytes = r.get("Bytes") or r.get("Size") or ""
+            nbytes = r.get("Bytes") or r.get("Size") or r.get("Copy_Bytes") or ""
             if nbytes:
                 kind += "(%.1fMB)" % (int(nbytes) / 1e6)
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind, r.get("Stream_Id", "?")))

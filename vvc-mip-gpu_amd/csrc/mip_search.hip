@@ -103,11 +103,7 @@ constexpr int kEntryBytes = 16;                         // 8 f16 MFMA inputs per
 constexpr int kCuTableBytes = 64 * kEntryBytes;
 constexpr int kScratchWords = 1280;                     // [slot][position] packed mode pairs
 constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
-#ifndef MIP_WAVE_STRIDE
-#define MIP_WAVE_STRIDE kWaveBytes  // LDS bytes between waves' private areas; smaller values
-                                    // overlap them (wrong results: occupancy-bound experiments)
-#endif
-constexpr int kWaveStride = MIP_WAVE_STRIDE;
+constexpr int kWaveStride = kWaveBytes;  // LDS bytes between waves' private areas
 constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 16;    // > every uniform B offset + 8 B
 constexpr int kUnavailable = 0x7fffffff;
 

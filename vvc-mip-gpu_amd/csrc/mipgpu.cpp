@@ -917,10 +917,29 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     hipError_t _e = hipMalloc((void **)&(ptr), (bytes));                                \
     if (_e != hipSuccess) return cleanup(fail("hipMalloc(%zu): %s", (size_t)(bytes), hipGetErrorString(_e))); \
   } while (0)
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess)
-    return cleanup(fail("hipStreamCreate failed"));
+  {
+    // The engine's streams are created with the device's greatest priority.  HIP maps streams
+    // onto a few hardware queues per priority (GPU_MAX_HW_QUEUES, 4 on the MI355X boxes); a
+    // process that already holds many streams of the default priority -- torch creates a pool
+    // of 32 per priority level at its first torch.cuda.Stream() -- then shares those queues
+    // with the engine's streams, and the host pipeline's downloads ran as blit kernels beside
+    // the searches: 8 queued 1-frame 1080p full-table calls 830 instead of 1000 frames/s,
+    // the configs[2] shape 570-894 instead of 1026 (tools/e2e_probe.py --torch stream,
+    // gpurun_out/r05l).  With an explicit priority both rates are restored (high or low alike;
+    // high, so that a serving engine is not starved by other work).  MIPGPU_STREAM_PRIO
+    // (A/B knob): "low" / "normal" (the plain default streams).
+    int lo = 0, hi = 0, prio = 0;
+    bool with_prio = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
+    prio = hi;
+    if (const char *sp = getenv("MIPGPU_STREAM_PRIO")) {
+      if (!strcmp(sp, "low")) prio = lo;
+      else if (!strcmp(sp, "normal")) with_prio = false;
+    }
+    for (hipStream_t *st : {&e->stream, &e->stream2, &e->stream3})
+      if ((with_prio ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio)
+                     : hipStreamCreateWithFlags(st, hipStreamNonBlocking)) != hipSuccess)
+        return cleanup(fail("hipStreamCreate failed"));
+  }
   // The slot events order the engine's own streams on this device only (uploads -> search ->
   // downloads; the kernels' dispatch packets carry the device-scope cache fences).
   // MIPGPU_SLOT_EVENTS (A/B knob): "nofence" drops their system-scope fences
