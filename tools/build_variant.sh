@@ -15,10 +15,11 @@ tmp=$(mktemp -d)
 trap 'rm -rf "$tmp"' EXIT
 id="$(make -s KNOBS="$*" build-id)"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc $*"
+pids=()
 for s in mip_search mip_filter mip_fixup; do
-  /opt/rocm/bin/hipcc $F -c -o "$tmp/$s.o" "csrc/$s.hip" &
+  /opt/rocm/bin/hipcc $F -c -o "$tmp/$s.o" "csrc/$s.hip" & pids+=($!)
 done
-/opt/rocm/bin/hipcc $F "-DMIPGPU_BUILD_ID=\"$id\"" -c -o "$tmp/mipgpu.o" csrc/mipgpu.cpp &
-wait
+/opt/rocm/bin/hipcc $F "-DMIPGPU_BUILD_ID=\"$id\"" -c -o "$tmp/mipgpu.o" csrc/mipgpu.cpp & pids+=($!)
+for p in "${pids[@]}"; do wait "$p" || { echo "build_variant: a compile failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$out" "$tmp"/*.o
 echo "built $out ($id)"

@@ -40,7 +40,15 @@ constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 1
                                       4, 4, 4, 8, 8, 8, 32, 16};
 constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4, 8, 16, 8, 16,
                                       32, 16, 8, 32, 16, 16, 16, 32};
-constexpr int kClassV[kNumClasses] = {4, 2, 1, 2, 1, 1, 1, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2, 4,
+// MIP_SIX_WAVES (round 5): 12-wave search workgroups, two per CU -- six waves per SIMD instead
+// of four (mip_search.hip: the MIP tables read from global memory, a smaller per-wave scratch,
+// 80 VGPRs); 16x16 and 16x8 CUs then take two row parts (their one-row-part tasks need 1168
+// scratch words).
+#ifndef MIP_SIX_WAVES
+#define MIP_SIX_WAVES 0
+#endif
+constexpr int kV16 = MIP_SIX_WAVES ? 2 : 1;  // row parts of the 16x16 / 16x8 base classes
+constexpr int kClassV[kNumClasses] = {4, 2, 1, 2, 1, 1, kV16, kV16, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2, 4,
                                       2, 2, 1, 1, 1, 4, 2, 4};
 constexpr bool kClassTR[kNumClasses] = {false, false, false, false, false, false, false, false, false, false, false,
                                         false, false, false, false, false, false, false, false, false, false,
@@ -175,7 +183,8 @@ struct FilterArgs {
 // Waves per search workgroup: two 8-wave workgroups share a CU in batched launches; small
 // launches can run one 16-wave workgroup per CU instead ("wide"), whose waves share one
 // item's tasks (launch_search).
-constexpr int kSearchWaves = 8, kWideWaves = 16;
+// (MIP_SIX_WAVES 1: two 12-wave workgroups per CU; 2: three 8-wave workgroups per CU)
+constexpr int kSearchWaves = MIP_SIX_WAVES == 1 ? 12 : 8, kWideWaves = 16;
 // Workgroups of the search kernel resident on the current device at once (persistent grid
 // size); computed once per engine (mip_engine_create), 0 on error.
 int search_resident_groups(bool alt_refs, bool wide);

@@ -90,6 +90,9 @@ __constant__ ShapeStarts c_shape_start = make_shape_starts();
 #ifndef MIP_ONLY_CLASS
 #define MIP_ONLY_CLASS -1  // resource census of one size class (tools/vgpr_census.sh)
 #endif
+#ifndef MIP_SKIP_CLASSES
+#define MIP_SKIP_CLASSES 0  // bit mask of size classes compiled out (occupancy experiments; wrong tables)
+#endif
 
 constexpr int kPitch = 68;       // LDS row pitch in samples (34 dwords: conflict-free rows)
 constexpr int kColOff = 4;       // LDS column of quadrant column 0 (-4..-1: left halo)
@@ -101,7 +104,11 @@ constexpr int kLatElems = (16 * kLatRowPitch + 16 * kLatColPitch + 7) / 8 * 8;
 // Wave-private LDS: per-CU MFMA inputs + reduced-prediction scratch.
 constexpr int kEntryBytes = 16;                         // 8 f16 MFMA inputs per CU
 constexpr int kCuTableBytes = 64 * kEntryBytes;
-constexpr int kScratchWords = 1280;                     // [slot][position] packed mode pairs
+#ifndef MIP_SCRATCH_WORDS
+// 1152 with six waves per SIMD: two 12-wave workgroups per CU in 160 KB of LDS
+#define MIP_SCRATCH_WORDS (MIP_SIX_WAVES == 1 ? 1152 : (MIP_SIX_WAVES == 2 ? 1144 : 1280))
+#endif
+constexpr int kScratchWords = MIP_SCRATCH_WORDS;        // [slot][position] packed mode pairs
 constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
 constexpr int kWaveStride = kWaveBytes;  // LDS bytes between waves' private areas
 constexpr int kZeroBytes = 7 * 8 * kEntryBytes + 16;    // > every uniform B offset + 8 B
@@ -200,7 +207,8 @@ struct Geo {
   static constexpr bool PAD = UH > 1;
   static constexpr int RP = PAD ? R + 1 : R;
   // scratch: [slot][PITCH] dwords; UH == 1 classes read 4 consecutive positions (16-B aligned)
-  static constexpr int PITCH = UH == 1 ? CPOS + 4 : R * RP + 1;
+  // (the 64-slot 4xN classes drop the 4-word pad when it does not fit: 64 x 20 > kScratchWords)
+  static constexpr int PITCH = UH == 1 ? (SLOTS * (CPOS + 4) <= kScratchWords ? CPOS + 4 : CPOS) : R * RP + 1;
   static constexpr int WBASE = SID == 2 ? 0 : (SID == 1 ? kWeightRowOffS1 : kWeightRowOffS0);
   static constexpr int MODES = SID == 2 ? 6 : (SID == 1 ? 8 : 16);
   static_assert(SLOTS * S * V == 64, "lanes");
@@ -1519,7 +1527,7 @@ __device__ __forceinline__ void dispatch_task(const Ctx &x, const RefTile<ALT> &
 #define MIP_CASE(idx, W, H)                                                \
   case idx:                                                                \
     static_assert(kClassW[idx] == W && kClassH[idx] == H, "class table");  \
-    if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)                       \
+    if constexpr ((MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx) && !((MIP_SKIP_CLASSES >> idx) & 1)) \
       run_task<W, H, kClassV[idx], ALT, DEC>(x, rt, task, lane);           \
     break;
     MIP_CASE(0, 64, 64) MIP_CASE(1, 32, 32) MIP_CASE(2, 32, 16) MIP_CASE(3, 16, 32)
@@ -1534,7 +1542,7 @@ __device__ __forceinline__ void dispatch_task(const Ctx &x, const RefTile<ALT> &
 #define MIP_CASE_TR(idx, W, H)                                                    \
   case idx:                                                                       \
     static_assert(kClassW[idx] == W && kClassH[idx] == H && kClassTR[idx], "class table"); \
-    if (MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx)                              \
+    if constexpr ((MIP_ONLY_CLASS < 0 || MIP_ONLY_CLASS == idx) && !((MIP_SKIP_CLASSES >> idx) & 1)) \
       run_task<W, H, kClassV[idx], ALT, DEC, true>(x, rt, task, lane);            \
     break;
     // transposed classes: wide CUs searched as their transposes
@@ -1657,21 +1665,30 @@ __device__ __forceinline__ void pair_loop(const SearchArgs &a, uint16_t *org_buf
 // DEC: decisions only -- no cost table, per-CU decisions (SearchArgs::best_mode / best_cost).
 // NW: waves per workgroup (kSearchWaves; kWideWaves: one workgroup per CU, small launches)
 #ifndef MIP_WAVES_PER_EU
-#define MIP_WAVES_PER_EU 4  // HIP-Clang: the second launch bound is the minimum waves per SIMD
+#define MIP_WAVES_PER_EU (MIP_SIX_WAVES ? 6 : 4)  // HIP-Clang: the second launch bound is the minimum waves per SIMD
 #endif
+// Six waves per SIMD: the MIP tables are read from global memory (L1 / L2) instead of LDS
+// and the search never prefetches the next window (no LDS for a second one).
+#ifndef MIP_TABLES_GLOBAL
+#define MIP_TABLES_GLOBAL 0  // A/B: the MIP tables from global memory at four waves per SIMD too
+#endif
+constexpr bool kTablesInLds = !MIP_SIX_WAVES && !MIP_TABLES_GLOBAL;
+constexpr bool kPrefetchKernel = !MIP_SIX_WAVES;
 template <bool ALT, bool DEC, bool PF_, int NW>
-__global__ __launch_bounds__(64 * NW, MIP_WAVES_PER_EU) void mip_search_kernel(SearchArgs a) {
-  constexpr bool PF = PF_ && !ALT && NW == kSearchWaves;
+__global__ __launch_bounds__(64 * NW, NW == kWideWaves ? 4 : MIP_WAVES_PER_EU) void mip_search_kernel(SearchArgs a) {
+  constexpr bool PF = PF_ && !ALT && NW == kSearchWaves && kPrefetchKernel;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *org_buf = reinterpret_cast<uint16_t *>(smem);  // kOrgTiles windows
   uint16_t *lattice = org_buf + kOrgTiles<ALT, PF, NW> * kTileElems;
-  uint8_t *w = smem + (kOrgTiles<ALT, PF, NW> * kTileElems + (ALT ? kLatElems : 0)) * 2;
-  uint8_t *zero = w + kTableBytes;
+  uint8_t *tab = smem + (kOrgTiles<ALT, PF, NW> * kTileElems + (ALT ? kLatElems : 0)) * 2;
+  uint8_t *zero = tab + (kTablesInLds ? kTableBytes : 0);
   uint8_t *waves = zero + kZeroBytes;
   uint32_t *counters = reinterpret_cast<uint32_t *>(waves + NW * kWaveStride);
+  const uint8_t *w = kTablesInLds ? tab : reinterpret_cast<const uint8_t *>(a.tables);
 
-  for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x)
-    reinterpret_cast<uint4 *>(w)[i] = a.tables[i];
+  if constexpr (kTablesInLds)
+    for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x)
+      reinterpret_cast<uint4 *>(tab)[i] = a.tables[i];
   for (int i = threadIdx.x; i < kZeroBytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(zero)[i] = make_uint4(0, 0, 0, 0);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1896,7 +1913,7 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
 
 size_t search_lds_bytes(bool alt, bool pf, int waves) {
   const bool two = (pf || waves == kWideWaves) && !alt;  // kOrgTiles
-  return (size_t)((two ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + kTableBytes + kZeroBytes +
+  return (size_t)((two ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + (kTablesInLds ? kTableBytes : 0) + kZeroBytes +
          (size_t)waves * kWaveStride + kCounterWords * 4;
 }
 
@@ -1920,7 +1937,10 @@ int search_resident_groups(bool alt, bool wide) {
   else
     per_cu = alt ? std::min(resident_per_cu<true, false, false, S>(), resident_per_cu<true, true, false, S>())
                  : std::min({resident_per_cu<false, false, false, S>(), resident_per_cu<false, true, false, S>(),
-                             resident_per_cu<false, false, true, S>(), resident_per_cu<false, true, true, S>()});
+#if MIP_PREFETCH_MIN_ITEMS < 1000000 && !MIP_SIX_WAVES  // (builds that never prefetch: the others' grid)
+                             resident_per_cu<false, false, true, S>(), resident_per_cu<false, true, true, S>()
+#endif
+                             });
   return per_cu >= 1 ? cus * per_cu : 0;
 }
 
@@ -1946,7 +1966,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const int groups = std::min<long long>(env && atoi(env) > 0 ? atoi(env) : resident, a.nitems);
   const bool dec = a.cost == nullptr;
   if (dec && (!a.best_cost || !a.dfill_begin)) return hipErrorInvalidValue;
-  const bool pf = !alt_refs && !wide && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
+  const bool pf = kPrefetchKernel && !alt_refs && !wide && a.nitems >= (uint32_t)MIP_PREFETCH_MIN_ITEMS * (uint32_t)groups;
   const size_t lds = search_lds_bytes(alt_refs, pf, wide ? kWideWaves : kSearchWaves);
   const dim3 grid(groups);
   constexpr int S = kSearchWaves, L = kWideWaves;
