@@ -30,71 +30,9 @@
 #include <thread>
 #include <vector>
 
+#include "copy_pool.h"
+
 namespace mipgpu {
-
-// Fixed pool of host threads for large memcpys (one job at a time, split evenly).
-class CopyPool {
- public:
-  explicit CopyPool(int n) {
-    for (int i = 0; i < n; i++) th_.emplace_back([this, i] { run(i); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto &t : th_) t.join();
-  }
-  // memcpy(dst, src, n) over all threads; returns when done.
-  void copy(void *dst, const void *src, size_t n) {
-    if (n < (4u << 20) || th_.empty()) {
-      memcpy(dst, src, n);
-      return;
-    }
-    std::unique_lock<std::mutex> lk(mu_);
-    dst_ = (char *)dst;
-    src_ = (const char *)src;
-    n_ = n;
-    pending_ = (int)th_.size();
-    gen_++;
-    cv_.notify_all();
-    done_.wait(lk, [&] { return pending_ == 0; });
-  }
-
- private:
-  void run(int i) {
-    unsigned seen = 0;
-    for (;;) {
-      char *d;
-      const char *s;
-      size_t n;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
-        d = dst_, s = src_, n = n_;
-      }
-      const size_t nt = th_.size(), per = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
-      const size_t o = (size_t)i * per;
-      if (o < n) memcpy(d + o, s + o, std::min(per, n - o));
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (--pending_ == 0) done_.notify_all();
-      }
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_;
-  bool stop_ = false;
-  unsigned gen_ = 0;
-  int pending_ = 0;
-  char *dst_ = nullptr;
-  const char *src_ = nullptr;
-  size_t n_ = 0;
-};
 
 class HostStage {
  public:
