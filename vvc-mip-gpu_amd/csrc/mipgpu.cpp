@@ -18,7 +18,7 @@
 
 #include "mip_kernels.h"
 #include "mip_tables.h"
-#include "host_stage.h"
+#include "host_stage_hip.h"
 #include "queue_ring.h"
 
 namespace {
@@ -900,6 +900,7 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
 
   mip_engine *e = new mip_engine();
   e->device = device;
+  e->stage.set_device(device);  // (the bounce ring's completion thread)
   e->width = width;
   e->height = height;
   e->nctus = mip_num_ctus(width, height);
@@ -1386,12 +1387,12 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     sb = std::max(1, std::min<int>(sb, (int)(cap / down_per_frame)));
   }
   const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
-  const bool pin_in = mipgpu::HostStage::pinned(frames) && (!refs_or_null || mipgpu::HostStage::pinned(refs_or_null));
-  const bool pin_cost = !costs_out || mipgpu::HostStage::pinned(costs_out);
-  const bool pin_sad = !sad_out || mipgpu::HostStage::pinned(sad_out);
-  const bool pin_satd = !satd_out || mipgpu::HostStage::pinned(satd_out);
-  const bool pin_bm = !best_mode_out || mipgpu::HostStage::pinned(best_mode_out);
-  const bool pin_bc = !best_cost_out || mipgpu::HostStage::pinned(best_cost_out);
+  const bool pin_in = mipgpu::host_pinned(frames) && (!refs_or_null || mipgpu::host_pinned(refs_or_null));
+  const bool pin_cost = !costs_out || mipgpu::host_pinned(costs_out);
+  const bool pin_sad = !sad_out || mipgpu::host_pinned(sad_out);
+  const bool pin_satd = !satd_out || mipgpu::host_pinned(satd_out);
+  const bool pin_bm = !best_mode_out || mipgpu::host_pinned(best_mode_out);
+  const bool pin_bc = !best_cost_out || mipgpu::host_pinned(best_cost_out);
   auto equal_chunks = [&] {  // a short last chunk would leave the search waiting for the next upload
     const int nch = (nframes + sb - 1) / sb;
     sb = (nframes + nch - 1) / nch;
