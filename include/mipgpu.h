@@ -130,8 +130,8 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
  * sad_out / satd_out: optional (need opts.want_sad_satd).  Synchronous.
  * Host buffers: page-locked memory (mip_host_alloc, hipHostRegister) is transferred by DMA
  * directly; pageable memory (malloc, the reference's return_minSadHad, main.cpp:656-668)
- * goes through the engine's page-locked bounce ring (16 pieces of up to 64 MB, parallel host
- * copies), allocated at its first use. */
+ * goes through the engine's page-locked bounce ring (one arena of 16 pieces of up to 64 MB,
+ * parallel host copies), allocated at its first use. */
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
                       int nframes, int32_t *costs_out, uint8_t *best_mode_out,
                       int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out);
@@ -147,8 +147,9 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
                             uint64_t *ticket);
 
 /* Block until the call with this ticket (and every earlier one) has completed: its outputs
- * are in host memory.  Pageable output buffers are written (copied out of the bounce ring)
- * by this call -- an asynchronous call with pageable outputs must be waited for.  Fails
+ * are in host memory.  Pageable output buffers are complete (copied out of the bounce ring by
+ * its completion thread) when this returns -- an asynchronous call with pageable outputs
+ * must be waited for.  Fails
  * if THIS call's search staged a sample above 1023 (input contract; every call has its own
  * status, so an earlier or later call's violation is reported by that call's own wait). */
 int mip_wait(mip_engine *e, uint64_t ticket);

@@ -2,7 +2,7 @@
 // three in-order "streams", each run by its own thread, execute the ring's copies and event
 // records after random delays, like DMA engines.  Checks that every download reaches its
 // pageable destination by the time drain(call) returns, that no piece is refilled before its
-// DMA has read it (uploads arrive intact), that a failing event wait is reported once by the
+// DMA has read it and no two live parts overlap in the arena (uploads arrive intact), that a failing event wait is reported once by the
 // next drain, and that abandon() / teardown with work in flight return with the ring idle
 // and reusable.  Built and run by tests/test_host_stage.py (g++, no GPU; also under
 // ThreadSanitizer when the compiler has it).
@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#define MIPGPU_RING_CHECK 1
 #include "host_stage.h"
 
 namespace {
@@ -152,7 +153,7 @@ void fill(std::vector<char> &v, uint32_t seed) {
 // Calls of random sizes: upload a pageable source into the call's "device" buffer, then
 // download it (same stream, so in order) into a pageable destination; the caller drains
 // calls a few behind, as mip_wait does, and checks each destination right after its drain.
-void round_trips(Sim &sim, std::atomic<int> &allocs, int ncalls, size_t piece, int lag) {
+void round_trips(Sim &sim, std::atomic<int> &allocs, int ncalls, size_t piece, int lag, size_t max_bytes = 0) {
   Ring ring(SimDev{&sim, &allocs});
   CHECK(ring.reserve(piece) == 0);
   std::mt19937 r(11);
@@ -162,7 +163,7 @@ void round_trips(Sim &sim, std::atomic<int> &allocs, int ncalls, size_t piece, i
   std::vector<Call> calls(ncalls);
   for (int c = 0; c < ncalls; c++) {
     Call &k = calls[c];
-    const size_t n = 1 + r() % (3 * ring.piece() + 12345);  // 1 .. several pieces
+    const size_t n = 1 + r() % (max_bytes ? max_bytes : 3 * ring.piece() + 12345);  // 1 .. several pieces
     k.src.resize(n);
     k.dev.assign(n, 0);
     k.dst.assign(n, 0);
@@ -181,6 +182,7 @@ void round_trips(Sim &sim, std::atomic<int> &allocs, int ncalls, size_t piece, i
     }
   }
   CHECK(ring.drain(~0ull) == 0);
+  CHECK(ring.bad_takes() == 0);
   for (int w = std::max(0, ncalls - lag); w < ncalls; w++) {
     std::vector<char> want(calls[w].dst.size());
     fill(want, 100 + w);
@@ -201,6 +203,9 @@ int main(int argc, char **argv) {
   sim.max_delay_us = 0;
   round_trips(sim, allocs, 200 / q, 1, 3);  // fast device: the completion thread races the caller
   sim.max_delay_us = 200;
+  round_trips(sim, allocs, 300 / q, 1, 40, 64u << 10);  // small parts: more in flight than events
+  round_trips(sim, allocs, 300 / q, 1, 12, 700u << 10);  // parts of mixed sizes: the arena wraps
+  round_trips(sim, allocs, 200 / q, 1, 30, 5u << 19);    // calls waiting for room (the ring retires parts)
   CHECK(allocs.load() == 0);
 
   {
@@ -210,7 +215,7 @@ int main(int argc, char **argv) {
     std::vector<char> src(3u << 20, 1), dev(3u << 20), dst(3u << 20);
     {
       std::lock_guard<std::mutex> lk(sim.mu);
-      sim.ev[sim.ev.size() - Ring::kRing + 2].fail_next = true;  // the upload's last piece
+      sim.ev[sim.ev.size() - Ring::kEvents + 2].fail_next = true;  // the upload's last piece
     }
     CHECK(ring.upload(dev.data(), src.data(), src.size(), 0, 1) == 0);
     CHECK(ring.download(dst.data(), dev.data(), dst.size(), 0, 2) == 0);
@@ -265,7 +270,7 @@ int main(int argc, char **argv) {
     CHECK(ring.download(dst.data(), dev.data(), dev.size(), 0, 1) == 0);
     CHECK(ring.reserve(4u << 20) == 0);
     CHECK(dst == dev);
-    CHECK(allocs.load() == Ring::kRing);
+    CHECK(allocs.load() == 1);  // (one arena)
   }
   CHECK(allocs.load() == 0);
 

@@ -1,5 +1,5 @@
 set -e
-O=gpurun_out/r05s; mkdir -p $O
+O=${O:-gpurun_out/r05s}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 F5=filterFrame_2d_float_5x5_quarterCtu

@@ -65,6 +65,12 @@ def torch_steps(step, W, H):
     torch.cuda.synchronize()
 
 
+def hip_runtimes():
+    """The HIP runtime libraries mapped into this process (torch's wheel bundles its own;
+    whichever is loaded first serves the engine)."""
+    return sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln})
+
+
 def run(case, W, H, calls, reps, torch_after=None, device_first=0):
     F, out, host, flt, kidx, mb = parse(case)
     src = synth_frames(W, H, min(F, 4), 0x1080, 0)
@@ -100,7 +106,7 @@ def run(case, W, H, calls, reps, torch_after=None, device_first=0):
             enq.append(1e3 * (t1 - t0))
             wt.append(1e3 * (t2 - t1))
             del tickets
-    return {"case": case, "frames_per_call": F, "out": out, "host": host, "filter": flt, "kernel_idx": kidx,
+    return {"case": case, "hip_runtime": hip_runtimes(), "frames_per_call": F, "out": out, "host": host, "filter": flt, "kernel_idx": kidx,
             "max_batch": mb, "calls": calls, "fps": round(float(np.median(rates)), 1),
             "fps_all": [round(r, 1) for r in rates], "enqueue_ms": [round(x, 3) for x in enq],
             "wait_ms": [round(x, 3) for x in wt]}

@@ -1,6 +1,6 @@
-// host_stage_hip.h -- the pageable bounce ring (host_stage.h) bound to HIP: page-locked
-// pieces from hipHostMalloc, DMAs with hipMemcpyAsync on the pipeline's streams, one
-// timing-free event per piece.
+// host_stage_hip.h -- the pageable bounce ring (host_stage.h) bound to HIP: one page-locked
+// arena from hipHostMalloc, DMAs with hipMemcpyAsync on the pipeline's streams, one
+// timing-free event per part in flight.
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -1405,20 +1405,20 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     const size_t per_frame = std::max({fs * 2, down_per_frame ? cpf * 4 : 0,
                                        best_cost_out ? upf * 4 : (best_mode_out ? upf : 0)});
     HIP_TRY(e->stage.reserve(std::min<size_t>((size_t)slot_cap * per_frame, mipgpu::HostStage::kMaxPiece)));
-    // Pageable transfers are cut into ring pieces per buffer: a chunk's downloads must fit
-    // the ring beside the next chunk's uploads (host_stage.h kMaxChunkPieces), else
-    // enqueueing them waits on the host for the chunk's own search.  Counted per buffer
-    // (each rounds up to whole pieces).
+    // Pageable transfers take ring bytes per buffer: a chunk's downloads must fit the ring
+    // beside the next chunk's uploads (host_stage.h kMaxChunkPieces), else enqueueing them
+    // waits on the host for the chunk's own search.
     const size_t piece = e->stage.piece();
-    auto pieces = [&](bool pinned, size_t bytes_per_frame) -> int {
-      return pinned || !bytes_per_frame ? 0 : (int)(((size_t)sb * bytes_per_frame + piece - 1) / piece);
+    auto bytes = [&](bool pinned, size_t bytes_per_frame) -> size_t {
+      return pinned ? 0 : e->stage.footprint((size_t)sb * bytes_per_frame);
     };
     auto fits = [&] {
-      const int down_p = pieces(pin_cost, costs_out ? cpf * 4 : 0) + pieces(pin_sad, sad_out ? cpf * 4 : 0) +
-                         pieces(pin_satd, satd_out ? cpf * 4 : 0) + pieces(pin_bm, best_mode_out ? upf : 0) +
-                         pieces(pin_bc, best_cost_out ? upf * 4 : 0);
-      const int up_p = pieces(pin_in, fs * 2) * (refs_or_null ? 2 : 1);
-      return down_p <= mipgpu::HostStage::kMaxChunkPieces && up_p <= mipgpu::HostStage::kRing - mipgpu::HostStage::kMaxChunkPieces;
+      const size_t down_b = bytes(pin_cost, costs_out ? cpf * 4 : 0) + bytes(pin_sad, sad_out ? cpf * 4 : 0) +
+                            bytes(pin_satd, satd_out ? cpf * 4 : 0) + bytes(pin_bm, best_mode_out ? upf : 0) +
+                            bytes(pin_bc, best_cost_out ? upf * 4 : 0);
+      const size_t up_b = bytes(pin_in, fs * 2) * (refs_or_null ? 2 : 1);
+      return down_b <= mipgpu::HostStage::kMaxChunkPieces * piece &&
+             up_b <= mipgpu::HostStage::kMaxChunkUploadPieces * piece;
     };
     while (sb > 1 && !fits()) sb--;
     equal_chunks();

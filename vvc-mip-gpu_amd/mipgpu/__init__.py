@@ -12,7 +12,9 @@ Mirrors the reference's operator surface (main.cpp + main_aux_functions.h):
 from __future__ import annotations
 
 import ctypes
+import importlib.util
 import os
+import sys
 import weakref
 
 import numpy as np
@@ -60,6 +62,25 @@ class _Opts(ctypes.Structure):
 _lib = None
 
 
+def _one_hip_runtime():
+    """One HIP runtime per process.  torch's ROCm wheel bundles its own libamdhip64 /
+    libhsa-runtime64 and loads them by path, so if libmipgpu.so were loaded first (binding
+    /opt/rocm's runtime) a later `import torch` would bring a second HIP and HSA runtime into
+    the process, and torch then finds no GPU once ours has opened it.  When torch is
+    installed it is imported first, and libmipgpu.so binds to the runtime torch loaded (same
+    soname).  MIPGPU_NO_TORCH=1 skips this (a process that never imports torch)."""
+    if "torch" in sys.modules or os.environ.get("MIPGPU_NO_TORCH"):
+        return
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
+def hip_runtimes():
+    """Paths of the HIP runtime libraries mapped into this process (diagnostic: one expected)."""
+    with open("/proc/self/maps") as f:
+        return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
+
+
 def library():
     """Load libmipgpu.so (raises if it was not built: the HIP path is mandatory)."""
     global _lib
@@ -68,6 +89,7 @@ def library():
     if not os.path.exists(LIB_PATH):
         raise MipError(f"{LIB_PATH} not found -- build it with `make -C vvc-mip-gpu_amd` "
                        "(or __graft_entry__.build()); there is no CPU fallback")
+    _one_hip_runtime()
     L = ctypes.CDLL(LIB_PATH)
     vp, ip, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
     sig = {
