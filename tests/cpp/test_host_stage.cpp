@@ -77,6 +77,7 @@ struct SimDev {
   using Stream = int;
   using Event = int;
   static constexpr Err kOk = 0;
+  static constexpr Err kNotReady = 3;
   Sim *sim;
   std::atomic<int> *allocs;
   Err host_alloc(char **p, size_t n) {
@@ -207,6 +208,15 @@ int main(int argc, char **argv) {
   round_trips(sim, allocs, 300 / q, 1, 12, 700u << 10);  // parts of mixed sizes: the arena wraps
   round_trips(sim, allocs, 200 / q, 1, 30, 5u << 19);    // calls waiting for room (the ring retires parts)
   CHECK(allocs.load() == 0);
+
+  {
+    // a transfer before reserve() is refused (no ring to stage through)
+    Ring ring(SimDev{&sim, &allocs});
+    std::vector<char> buf(100), dev(100);
+    CHECK(ring.upload(dev.data(), buf.data(), buf.size(), 0, 1) == SimDev::kNotReady);
+    CHECK(ring.download(buf.data(), dev.data(), dev.size(), 0, 1) == SimDev::kNotReady);
+    CHECK(ring.idle());
+  }
 
   {
     // a failing event wait: reported once, by the drain that covers it; the ring goes on

@@ -41,7 +41,8 @@
 
 namespace mipgpu {
 
-// Dev provides: types Err, Stream, Event; static constexpr Err kOk; and
+// Dev provides: types Err, Stream, Event; static constexpr Err kOk, kNotReady (a transfer
+// before reserve()); and
 //   Err host_alloc(char **p, size_t n);        void host_free(char *p);
 //   Err event_create(Event *e);                void event_destroy(Event e);
 //   Err copy_h2d(void *dev, const void *host, size_t n, Stream s);
@@ -133,6 +134,7 @@ class BounceRing {
 
   // Pageable host -> device on stream s (the source is copied before this returns).
   Err upload(void *dst_dev, const void *src, size_t n, Stream s, uint64_t call) {
+    if (!piece_) return Dev::kNotReady;
     for (size_t o = 0; o < n; o += piece_) {
       const size_t len = std::min(piece_, n - o);
       Piece p{0, len, nullptr, call, 0, false};
@@ -153,6 +155,7 @@ class BounceRing {
   // Device -> pageable host on stream s; the host side is written by the completion thread
   // (complete for every call <= c once drain(c) returns).
   Err download(void *dst, const void *src_dev, size_t n, Stream s, uint64_t call) {
+    if (!piece_) return Dev::kNotReady;
     for (size_t o = 0; o < n; o += piece_) {
       const size_t len = std::min(piece_, n - o);
       Piece p{0, len, (char *)dst + o, call, 0, false};

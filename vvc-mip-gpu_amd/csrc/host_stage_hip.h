@@ -13,6 +13,7 @@ struct HipStageDev {
   using Stream = hipStream_t;
   using Event = hipEvent_t;
   static constexpr Err kOk = hipSuccess;
+  static constexpr Err kNotReady = hipErrorNotInitialized;
   Err host_alloc(char **p, size_t n) { return hipHostMalloc((void **)p, n, hipHostMallocDefault); }
   void host_free(char *p) { (void)hipHostFree(p); }
   Err event_create(Event *e) { return hipEventCreateWithFlags(e, hipEventDisableTiming); }

@@ -923,8 +923,10 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     // onto a few hardware queues per priority (GPU_MAX_HW_QUEUES, 4 on the MI355X boxes); a
     // process that already holds many streams of the default priority -- torch creates a pool
     // of 32 per priority level at its first torch.cuda.Stream() -- then shares those queues
-    // with the engine's streams, and the host pipeline's downloads ran as blit kernels beside
-    // the searches: 8 queued 1-frame 1080p full-table calls 830 instead of 1000 frames/s,
+    // with the engine's streams, and the host pipeline's downloads -- blit kernels on the
+    // runtime torch's wheel bundles, which then serves the engine (DESIGN.md section 6,
+    // pageable host buffers, round 5) -- queued behind the searches on a shared queue:
+    // 8 queued 1-frame 1080p full-table calls 830 instead of 1000 frames/s,
     // the configs[2] shape 570-894 instead of 1026 (tools/e2e_probe.py --torch stream,
     // gpurun_out/r05l).  With an explicit priority both rates are restored (high or low alike;
     // high, so that a serving engine is not starved by other work).  MIPGPU_STREAM_PRIO
