@@ -331,6 +331,30 @@ def test_host_pipeline_four_slots_uneven_chunks(gpu_available, filt, k):
         assert np.array_equal(host["best_cost"][f], bc), f
 
 
+@pytest.mark.parametrize("filt,k", [(None, 0), ("filterFrame_2d_float_5x5_quarterCtu", 2)])
+def test_host_pipeline_ramped_first_chunks(gpu_available, filt, k):
+    """A call into an idle pipeline with max_batch 64 (4 slots of 16 frames) ramps its first
+    chunks up (4, 7, 12 frames, then 14 + 14 + 13: mipgpu.cpp search_frames_chunks), a call
+    queued behind it does not; full tables + decisions, then decisions only.  Every frame must
+    equal the oracle."""
+    w, h, n = 136, 72, 64
+    frames = synth_frames(w, h, n, 0x7A3, 0)
+    nct = layout.num_ctus(w, h)
+    want = [O.engine_search(frames[f], filt, k) for f in range(n)]
+    with MipEngine(w, h, max_batch=n, filter=filt, kernel_idx=k) as eng:
+        t1 = eng.search_async(frames, best=True)
+        t2 = eng.search_async(frames[::-1].copy(), best=True)
+        r1, r2 = eng.wait(t1), eng.wait(t2)
+        dec = eng.search(frames, costs=False, best=True)
+    for f in range(n):
+        bm, bc = layout.best_modes(want[f], nct)
+        assert np.array_equal(r1["cost"][f], want[f]), f
+        assert np.array_equal(r2["cost"][n - 1 - f], want[f]), f
+        assert np.array_equal(r1["best_mode"][f], bm), f
+        assert np.array_equal(dec["best_mode"][f], bm), f
+        assert np.array_equal(dec["best_cost"][f], bc), f
+
+
 def test_engine_filter_scratch_shared_by_two_streams(gpu_available):
     """Device-API searches that filter into the engine's reference scratch (no caller
     references) on two streams, with different frames per launch: each launch must wait

@@ -1372,11 +1372,9 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // A call into an idle pipeline (nothing queued before it) is cut in two, so that its own
   // upload, search and download overlap; calls queued behind others keep whole-call chunks
   // (the overlap comes from the neighbouring calls, and larger launches are more efficient).
-  if (nslots == 3 && nframes >= 2) {
-    const bool idle = e->host_calls == 0 ||
-                      hipEventQuery(e->call_done[(e->host_calls - 1) % mip_engine::kCallRing]) == hipSuccess;
-    if (idle) sb = (nframes + 1) / 2;
-  }
+  const bool idle = e->host_calls == 0 ||
+                    hipEventQuery(e->call_done[(e->host_calls - 1) % mip_engine::kCallRing]) == hipSuccess;
+  if (nslots == 3 && nframes >= 2 && idle) sb = (nframes + 1) / 2;
   // Full tables to the host (PCIe-bound): chunks of at most ~1 GiB of downloads, so the
   // first download starts early and, for pageable outputs, the bounce ring's copy-out keeps
   // up (1080p, 8 calls of 128 frames: 96-frame chunks 831 frames/s pageable, 32-frame 892,
@@ -1432,8 +1430,26 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   auto to_host = [&](void *h, const void *d, size_t n, bool pinned) {
     return pinned ? hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, down) : e->stage.download(h, d, n, down, call);
   };
-  for (int f0 = 0; f0 < nframes; f0 += sb) {
-    const int nb = std::min(sb, nframes - f0);
+  // A longer call into an idle pipeline ramps its first chunks up from a few frames: the
+  // search starts after one small upload instead of a whole chunk's (64 frames: 4.7 ms at
+  // 56 GB/s), and each chunk's upload still fits under the previous chunk's search (upload
+  // 74 us per 1080p frame, search ~131 us: growth x1.75); the rest of the call keeps equal
+  // chunks of at most sb.  MIPGPU_RAMP=0 (A/B knob): no ramp.
+  std::vector<int> plan;
+  {
+    int left = nframes;
+    const char *rv = getenv("MIPGPU_RAMP");
+    if (idle && nslots == 4 && sb >= 16 && nframes >= 2 * sb && !(rv && !strcmp(rv, "0"))) {
+      for (int c = 4; c < sb && left > sb + c; c = c * 7 / 4) {
+        plan.push_back(c);
+        left -= c;
+      }
+    }
+    const int nch = (left + sb - 1) / sb, per = (left + nch - 1) / nch;
+    for (int f = 0; f < left; f += per) plan.push_back(std::min(per, left - f));
+  }
+  int f0 = 0;
+  for (const int nb : plan) {
     const uint64_t k = e->host_chunks++;
     const int sl = (int)(k % nslots);
     const bool reuse = k >= (uint64_t)nslots;  // the slot served chunk k - nslots (this or an earlier call)
@@ -1503,6 +1519,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     if (best_mode_out) HIP_TRY(to_host(best_mode_out + f0 * upf, d_best, nb * upf, pin_bm));
     if (best_cost_out) HIP_TRY(to_host(best_cost_out + f0 * upf, d_best_cost, nb * upf * 4, pin_bc));
     HIP_TRY(hipEventRecord(e->slot_down[sl], down));
+    f0 += nb;
   }
   return 0;
 }
