@@ -5,6 +5,8 @@ of H2D, filter, search and D2H; tools/trace_timeline.py summarises such a trace)
 
     python tools/e2e_probe.py [--calls 8] [--reps 3] CASE [CASE ...]
 
+    python tools/e2e_probe.py --sync ... (synchronous calls one after the other)
+
 CASE = FRAMES:OUT:HOST[:FILTER:KIDX][:mb=MAX_BATCH]
   FRAMES  frames per call (1080p unless --width/--height)
   OUT     dec (per-CU best mode + cost only) | full (int32 cost table)
@@ -71,7 +73,7 @@ def hip_runtimes():
     return sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln})
 
 
-def run(case, W, H, calls, reps, torch_after=None, device_first=0):
+def run(case, W, H, calls, reps, torch_after=None, device_first=0, sync=False):
     F, out, host, flt, kidx, mb = parse(case)
     src = synth_frames(W, H, min(F, 4), 0x1080, 0)
     alloc = (lambda shape, dt: pinned_empty(shape, dt)) if host == "pinned" else (lambda shape, dt: np.zeros(shape, dt))
@@ -98,16 +100,22 @@ def run(case, W, H, calls, reps, torch_after=None, device_first=0):
         rates, enq, wt = [], [], []
         for _ in range(reps):
             t0 = time.perf_counter()
-            tickets = [eng.search_async(frames, **kw) for _ in range(calls)]
-            t1 = time.perf_counter()
-            eng.wait(tickets[-1])
-            t2 = time.perf_counter()
+            if sync:  # synchronous calls one after the other (mip_search_frames)
+                for _ in range(calls):
+                    eng.search(frames, **kw)
+                tickets = []
+                t1 = t2 = time.perf_counter()
+            else:
+                tickets = [eng.search_async(frames, **kw) for _ in range(calls)]
+                t1 = time.perf_counter()
+                eng.wait(tickets[-1])
+                t2 = time.perf_counter()
             rates.append(calls * F / (t2 - t0))
             enq.append(1e3 * (t1 - t0))
             wt.append(1e3 * (t2 - t1))
             del tickets
     return {"case": case, "hip_runtime": hip_runtimes(), "frames_per_call": F, "out": out, "host": host, "filter": flt, "kernel_idx": kidx,
-            "max_batch": mb, "calls": calls, "fps": round(float(np.median(rates)), 1),
+            "max_batch": mb, "calls": calls, "sync": sync, "fps": round(float(np.median(rates)), 1),
             "fps_all": [round(r, 1) for r in rates], "enqueue_ms": [round(x, 3) for x in enq],
             "wait_ms": [round(x, 3) for x in wt]}
 
@@ -121,12 +129,13 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--torch", default="", help="torch_steps(STEP) before the engines are created")
     ap.add_argument("--torch-after", default="", help="torch_steps(STEP) after each engine is created")
+    ap.add_argument("--sync", action="store_true", help="synchronous calls (mip_search_frames) instead of queued ones")
     ap.add_argument("--device-first", type=int, default=0, help="device-API searches of the engine first")
     a = ap.parse_args()
     if a.torch:
         torch_steps(a.torch, a.width, a.height)
     for c in a.cases:
-        print(json.dumps(run(c, a.width, a.height, a.calls, a.reps, a.torch_after, a.device_first)), flush=True)
+        print(json.dumps(run(c, a.width, a.height, a.calls, a.reps, a.torch_after, a.device_first, a.sync)), flush=True)
         time.sleep(0.2)
 
 

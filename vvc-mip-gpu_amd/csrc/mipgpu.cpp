@@ -1280,7 +1280,7 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
 
 static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                                 int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
-                                int32_t *satd_out, uint64_t call);
+                                int32_t *satd_out, uint64_t call, bool sync);
 
 // mip_trace_times: read the pending chunk times of slot `sl` (waits for its events).
 static int drain_trace(mip_engine *e, int sl) {
@@ -1298,9 +1298,11 @@ static int drain_trace(mip_engine *e, int sl) {
   return 0;
 }
 
-int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
-                            int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
-                            int32_t *satd_out, uint64_t *ticket) {
+// One host-API call (mip_search_frames_async; mip_search_frames with sync = true: it waits for
+// the call before returning, so no later call can queue behind its last chunks).
+static int search_frames_call(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
+                              int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
+                              int32_t *satd_out, uint64_t *ticket, bool sync) {
   if (!e || !frames || nframes < 1 || !ticket) return fail("bad search arguments");
   *ticket = 0;
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
@@ -1313,7 +1315,7 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
     harvest_status(e, next - mip_engine::kCallRing);
   }
   const int rc = search_frames_chunks(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out,
-                                      sad_out, satd_out, next);
+                                      sad_out, satd_out, next, sync);
   // After a failure part-way through the chunks, the chunks already queued are waited for
   // here (no ticket covers them).
   if (rc != 0) {
@@ -1340,9 +1342,16 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
   return 0;
 }
 
+int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
+                            int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
+                            int32_t *satd_out, uint64_t *ticket) {
+  return search_frames_call(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out, sad_out,
+                            satd_out, ticket, false);
+}
+
 static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                                 int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
-                                int32_t *satd_out, uint64_t call) {
+                                int32_t *satd_out, uint64_t call, bool sync) {
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
     HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
@@ -1433,20 +1442,28 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // A longer call into an idle pipeline ramps its first chunks up from a few frames: the
   // search starts after one small upload instead of a whole chunk's (64 frames: 4.7 ms at
   // 56 GB/s), and each chunk's upload still fits under the previous chunk's search (upload
-  // 74 us per 1080p frame, search ~131 us: growth x1.75); the rest of the call keeps equal
-  // chunks of at most sb.  MIPGPU_RAMP=0 (A/B knob): no ramp.
-  std::vector<int> plan;
+  // 74 us per 1080p frame, search ~131 us: growth x1.75).  A synchronous decisions-only call
+  // (mip_search_frames: nothing can queue behind it) ramps its last chunks down the same way,
+  // so the download left after the last search is a few frames' (decision lists: 67 us per
+  // frame, under the next chunk's search; full tables are download-bound throughout, where a
+  // ramp-down changes nothing).  The rest of the call keeps equal chunks of at most sb.
+  // MIPGPU_RAMP=0 (A/B knob): no ramps; MIPGPU_RAMP=up: no ramp-down.
+  std::vector<int> plan, tail;
   {
     int left = nframes;
     const char *rv = getenv("MIPGPU_RAMP");
-    if (idle && nslots == 4 && sb >= 16 && nframes >= 2 * sb && !(rv && !strcmp(rv, "0"))) {
+    const bool ramps = nslots == 4 && sb >= 16 && !(rv && !strcmp(rv, "0"));
+    auto ramp = [&](std::vector<int> &v) {
       for (int c = 4; c < sb && left > sb + c; c = c * 7 / 4) {
-        plan.push_back(c);
+        v.push_back(c);
         left -= c;
       }
-    }
+    };
+    if (ramps && idle && nframes >= 2 * sb) ramp(plan);
+    if (ramps && sync && !down_per_frame && !(rv && !strcmp(rv, "up")) && left > sb) ramp(tail);
     const int nch = (left + sb - 1) / sb, per = (left + nch - 1) / nch;
     for (int f = 0; f < left; f += per) plan.push_back(std::min(per, left - f));
+    plan.insert(plan.end(), tail.rbegin(), tail.rend());
   }
   int f0 = 0;
   for (const int nb : plan) {
@@ -1549,8 +1566,8 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
                       int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
                       int32_t *satd_out) {
   uint64_t ticket = 0;
-  if (mip_search_frames_async(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out, sad_out,
-                              satd_out, &ticket) != 0)
+  if (search_frames_call(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out, sad_out,
+                         satd_out, &ticket, true) != 0)
     return -1;
   return mip_wait(e, ticket);
 }

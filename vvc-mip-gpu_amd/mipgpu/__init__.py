@@ -257,12 +257,27 @@ class MipEngine:
         (decision lists [F, nCTUs*5380, K] when the engine has best_k = K > 1), 'sad' / 'satd'.
         `out` may supply any of these arrays (e.g. from pinned_empty, for DMA-rate
         transfers); the others are allocated."""
-        return self.wait(self.search_async(frames, refs, costs, best, sad_satd, out))
+        f, r, n, res = self._prepare(frames, refs, costs, best, sad_satd, out)
+        with self._lock:  # mip_search_frames: one synchronous call (its last chunks may ramp down)
+            _check(library().mip_search_frames(self._h, _ptr(f), _ptr(r), n, _ptr(res.get("cost")),
+                                               _ptr(res.get("best_mode")), _ptr(res.get("best_cost")),
+                                               _ptr(res.get("sad")), _ptr(res.get("satd"))))
+        return res
 
     def search_async(self, frames, refs=None, costs=True, best=False, sad_satd=False, out=None):
         """As search(), without waiting (mip_search_frames_async): the call queues behind
         the calls in flight and returns a ticket; wait(ticket) returns the output dict.  The
         ticket keeps the input and output arrays alive until then."""
+        f, r, n, res = self._prepare(frames, refs, costs, best, sad_satd, out)
+        t = ctypes.c_uint64()
+        with self._lock:
+            _check(library().mip_search_frames_async(self._h, _ptr(f), _ptr(r), n, _ptr(res.get("cost")),
+                                                     _ptr(res.get("best_mode")), _ptr(res.get("best_cost")),
+                                                     _ptr(res.get("sad")), _ptr(res.get("satd")), ctypes.byref(t)))
+        return _Ticket(t.value, res, (f, r), self)
+
+    def _prepare(self, frames, refs, costs, best, sad_satd, out):
+        """Input arrays and the output dict of a host search (allocated unless in `out`)."""
         f = self._frames(frames)
         r = None if refs is None else self._frames(refs)
         n = f.shape[0]
@@ -288,12 +303,7 @@ class MipEngine:
             a = buf(key, want, cols, dt)
             if a is not None:
                 res[key] = a
-        t = ctypes.c_uint64()
-        with self._lock:
-            _check(library().mip_search_frames_async(self._h, _ptr(f), _ptr(r), n, _ptr(res.get("cost")),
-                                                     _ptr(res.get("best_mode")), _ptr(res.get("best_cost")),
-                                                     _ptr(res.get("sad")), _ptr(res.get("satd")), ctypes.byref(t)))
-        return _Ticket(t.value, res, (f, r), self)
+        return f, r, n, res
 
     def wait(self, ticket):
         """Block until an asynchronous search has completed; returns its output dict."""
