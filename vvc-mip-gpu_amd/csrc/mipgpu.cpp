@@ -486,10 +486,11 @@ bool filter_valid(int f, int k) {
 struct mip_engine {
   int device = 0, width = 0, height = 0, nctus = 0, ctu_cols = 0;
   mip_opts opts{};
-  // Host API pipeline (mip_search_frames): `stream` computes, `stream2` uploads, `stream3`
-  // downloads; per buffer slot, events order upload -> compute -> download and a slot's
-  // reuse after its previous chunk (see mip_search_frames).
-  hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+  // Host API pipeline (mip_search_frames): `stream` and `stream4` compute (chunks alternate
+  // between them, so that one chunk's search takes the CUs its predecessor's drains), `stream2`
+  // uploads, `stream3` downloads; per buffer slot, events order upload -> compute -> download
+  // and a slot's reuse after its previous chunk (see mip_search_frames).
+  hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
   // Buffer slots of the host pipeline: hp_slots regions of hp_cap frames each in the engine
   // buffers (d_frames, d_refs, d_costs, ...).  Large engines (max_batch >= 16): 4 slots of a
   // quarter of max_batch; small ones: 3 slots of max_batch frames (triple buffering, so that a
@@ -568,12 +569,13 @@ struct mip_engine {
   static constexpr int kQueueSlots = 16;
   uint32_t *d_queue = nullptr;
   hipEvent_t queue_done[kQueueSlots] = {};
-  // Two rings: `queue` for device-API launches (any caller stream: reuse ordered by the
-  // slot's event) and `hp_queue` for the host pipeline, whose searches all run on the engine's
-  // own search stream `stream`: launches on one in-order stream never overlap, so its ring
-  // needs neither the event record nor the wait (two fewer queue packets per chunk on the
-  // search stream's critical path).  The pairs are distinct memory (hp_queue: slots
-  // kQueueSlots..2 kQueueSlots-1 of d_queue).
+  // Three rings: `queue` for device-API launches (any caller stream: reuse ordered by the
+  // slot's event) and `hp_queue` / `hp_queue2` for the host pipeline, whose searches run on
+  // the engine's own search streams `stream` / `stream4`, one ring each: launches on one
+  // in-order stream never overlap, so such a ring needs neither the event record nor the
+  // wait (two fewer queue packets per chunk on the search stream's critical path).  The pairs
+  // are distinct memory (hp_queue: slots kQueueSlots..2 kQueueSlots-1 of d_queue, hp_queue2
+  // the next kQueueSlots).
   struct QueueOps {
     mip_engine *e;
     int base;           // first counter pair of the ring in d_queue
@@ -592,6 +594,7 @@ struct mip_engine {
   };
   QueueRing<QueueOps, kQueueSlots> queue{QueueOps{this, 0, false}};
   QueueRing<QueueOps, kQueueSlots> hp_queue{QueueOps{this, kQueueSlots, true}};
+  QueueRing<QueueOps, kQueueSlots> hp_queue2{QueueOps{this, 2 * kQueueSlots, true}};  // (stream4)
   // Input contract (10-bit samples): status words the search kernel sets when it stages a
   // sample above 1023 (SearchArgs::status), in page-locked host memory mapped into the
   // device.  One set of kStatusWords per host-API call (call c: set (c - 1) % kCallRing) and
@@ -629,6 +632,13 @@ bool dec_inline() {
 bool ext_done_enabled() {
   const char *e = getenv("MIPGPU_EXT_DONE");
   return !(e && *e == '0');
+}
+
+// Host pipeline search streams: 2 (chunks alternate between `stream` and `stream4`) or 1
+// (MIPGPU_SEARCH_STREAMS=1, A/B knob: every search on `stream`).
+int search_streams() {
+  const char *e = getenv("MIPGPU_SEARCH_STREAMS");
+  return e && *e == '1' ? 1 : 2;
 }
 
 bool lpt_order_enabled() {
@@ -758,6 +768,7 @@ static void harvest_status(mip_engine *e, uint64_t upto) {
 static int wait_refs_readers(mip_engine *e) {
   if (!e->refs_pending) return 0;
   HIP_TRY(hipStreamWaitEvent(e->stream, e->refs_done, 0));
+  HIP_TRY(hipStreamWaitEvent(e->stream4, e->refs_done, 0));
   HIP_TRY(hipStreamWaitEvent(e->stream2, e->refs_done, 0));
   return 0;
 }
@@ -834,6 +845,7 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   if (e->stream3) (void)hipStreamSynchronize(e->stream3);
+  if (e->stream4) (void)hipStreamSynchronize(e->stream4);
   e->stage.abandon();
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_split_acc,
@@ -864,6 +876,7 @@ int mip_engine_destroy(mip_engine *e) {
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
   if (e->stream3) (void)hipStreamDestroy(e->stream3);
+  if (e->stream4) (void)hipStreamDestroy(e->stream4);
   delete e;
   return 0;
 }
@@ -938,7 +951,7 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
       if (!strcmp(sp, "low")) prio = lo;
       else if (!strcmp(sp, "normal")) with_prio = false;
     }
-    for (hipStream_t *st : {&e->stream, &e->stream2, &e->stream3})
+    for (hipStream_t *st : {&e->stream, &e->stream2, &e->stream3, &e->stream4})
       if ((with_prio ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio)
                      : hipStreamCreateWithFlags(st, hipStreamNonBlocking)) != hipSuccess)
         return cleanup(fail("hipStreamCreate failed"));
@@ -965,8 +978,8 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     ALLOC(e->d_satd, ncost * 4);
   }
   ALLOC(e->d_best, ncu * o.best_k);
-  ALLOC(e->d_queue, mipgpu::kQueueWords * 2 * mip_engine::kQueueSlots * sizeof(uint32_t));
-  if (hipMemset(e->d_queue, 0, mipgpu::kQueueWords * 2 * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
+  ALLOC(e->d_queue, mipgpu::kQueueWords * 3 * mip_engine::kQueueSlots * sizeof(uint32_t));
+  if (hipMemset(e->d_queue, 0, mipgpu::kQueueWords * 3 * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail("hipMemset failed"));
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
@@ -1205,9 +1218,9 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
                              e->nctus, ctu0, nrange, work.max_split, a.split_acc};
   if (defer_split) *defer_split = sa;
   if (decisions_only && !defer_split) HIP_TRY(mipgpu::launch_dec_split(sa, nframes, true, s));
-  // the host pipeline's launches (all on the engine's search stream) use their own ring
-  auto &ring = s == e->stream ? e->hp_queue : e->queue;
-  const int qbase = s == e->stream ? mip_engine::kQueueSlots : 0;
+  // the host pipeline's launches (on the engine's search streams) use their own rings
+  auto &ring = s == e->stream ? e->hp_queue : s == e->stream4 ? e->hp_queue2 : e->queue;
+  const int qbase = s == e->stream ? mip_engine::kQueueSlots : s == e->stream4 ? 2 * mip_engine::kQueueSlots : 0;
   const int slot = ring.acquire(s);
   if (slot < 0) return fail("ordering the search's item counter failed: %s", hipGetErrorString(hipGetLastError()));
   a.queue = e->d_queue + mipgpu::kQueueWords * (qbase + slot);
@@ -1322,6 +1335,7 @@ static int search_frames_call(mip_engine *e, const uint16_t *frames, const uint1
     const std::string err = g_err;
     (void)hipStreamSynchronize(e->stream2);
     (void)hipStreamSynchronize(e->stream);
+    (void)hipStreamSynchronize(e->stream4);
     (void)hipStreamSynchronize(e->stream3);
     // staged downloads of the calls before this one complete normally; this call's are dropped
     (void)e->stage.drain(e->host_calls);
@@ -1395,7 +1409,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     const size_t cap = (size_t)(cm && atoi(cm) > 0 ? atoi(cm) : 1024) << 20;
     sb = std::max(1, std::min<int>(sb, (int)(cap / down_per_frame)));
   }
-  const hipStream_t up = e->stream2, comp = e->stream, down = e->stream3;
+  const hipStream_t up = e->stream2, down = e->stream3;
   const bool pin_in = mipgpu::host_pinned(frames) && (!refs_or_null || mipgpu::host_pinned(refs_or_null));
   const bool pin_cost = !costs_out || mipgpu::host_pinned(costs_out);
   const bool pin_sad = !sad_out || mipgpu::host_pinned(sad_out);
@@ -1449,6 +1463,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // ramp-down changes nothing).  The rest of the call keeps equal chunks of at most sb.
   // MIPGPU_RAMP=0 (A/B knob): no ramps; MIPGPU_RAMP=up: no ramp-down.
   std::vector<int> plan, tail;
+  bool ramped = false;
   {
     int left = nframes;
     const char *rv = getenv("MIPGPU_RAMP");
@@ -1460,15 +1475,25 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
       }
     };
     if (ramps && idle && nframes >= 2 * sb) ramp(plan);
+    const bool head_empty = plan.empty();
     if (ramps && sync && !down_per_frame && !(rv && !strcmp(rv, "up")) && left > sb) ramp(tail);
     const int nch = (left + sb - 1) / sb, per = (left + nch - 1) / nch;
     for (int f = 0; f < left; f += per) plan.push_back(std::min(per, left - f));
+    ramped = !tail.empty() || !head_empty;
     plan.insert(plan.end(), tail.rbegin(), tail.rend());
   }
+  // Searches of consecutive chunks alternate between two search streams, so that a chunk's
+  // search takes the CUs as its predecessor's persistent grid drains -- except in ramped
+  // calls, whose short chunks are sized to run one after the other (device API, 1080p,
+  // tools/overlap_probe.py: one-frame launches +10 % decisions-only / +5 % full tables on
+  // two streams; host pipeline: 8 queued one-frame calls decisions-only +5 %, 4-frame +4 %,
+  // one synchronous ramped 128-frame call -2 %, so ramped calls keep one stream).
+  const bool alt_streams = search_streams() == 2 && !ramped;
   int f0 = 0;
   for (const int nb : plan) {
     const uint64_t k = e->host_chunks++;
     const int sl = (int)(k % nslots);
+    const hipStream_t comp = alt_streams && (k & 1) ? e->stream4 : e->stream;
     const bool reuse = k >= (uint64_t)nslots;  // the slot served chunk k - nslots (this or an earlier call)
     const size_t fo = (size_t)sl * slot_cap;  // first engine frame of this chunk's slot
     uint16_t *d_frames = e->d_frames + fo * fs;
@@ -1634,6 +1659,7 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
   // asynchronous host searches still in flight use d_frames / d_refs: let them finish
   HIP_TRY(hipStreamSynchronize(e->stream2));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream4));
   HIP_TRY(hipStreamSynchronize(e->stream3));
   for (int f0 = 0; f0 < nframes; f0 += e->opts.max_batch) {
     const int nb = std::min(e->opts.max_batch, nframes - f0);
