@@ -18,6 +18,9 @@ from mipgpu.synth import synth_frames  # noqa: E402
 
 W, H = 1920, 1080
 torch.cuda.init()
+if os.environ.get("NO_GC"):  # is a spike Python's garbage collector?
+    import gc
+    gc.disable()
 src = synth_frames(W, H, 1, 0x1080, 0)
 fr = pinned_empty((1, H, W), np.uint16)
 fr[:] = src
