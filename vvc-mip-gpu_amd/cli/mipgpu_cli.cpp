@@ -51,7 +51,7 @@ const char *kFilters[] = {"filterFrame_1d_int", "filterFrame_1d_float", "filterF
                           "filterFrame_2d_int_5x5_quarterCtu", "filterFrame_2d_float_5x5_quarterCtu"};
 
 struct Options {
-  int frames = -1, kernel_idx = 0, batch = 8, threads = 0, topk = 1;
+  int frames = -1, kernel_idx = 0, batch = 0, threads = 0, topk = 1;  // batch 0: auto
   std::vector<int> devices{0};
   std::string device_arg = "0";
   bool device_set = false, prefix_set = false, kidx_set = false, help = false;
@@ -84,7 +84,7 @@ void usage() {
                "  --ReportSadSatd                   Log real SAD/SATD columns (reference: MAX_PERFORMANCE_DIST=0)\n"
                "  --AllFrames                       Log every frame (reference logs frame 0 only)\n"
                "  --BestModes arg                   Write the per-CU best mode / cost to this CSV\n"
-               "  --BatchFrames arg (=8)            Frames per device batch\n"
+               "  --BatchFrames arg (=auto)         Frames per device batch (auto: ~256 MB of samples, at most 32)\n"
                "  --Threads arg (=0)                CSV parsing / log-formatting threads (0 = all cores)\n"
                "  --TopK arg (=1)                   Modes per CU in the BestModes file (1..32, ranked)\n"
                "  --BinaryLog arg                   Write every frame's int32 cost table to this file\n"
@@ -114,7 +114,7 @@ int set_opt(Options &o, const std::string &name, const std::string &val) {
     else if (name == "AllFrames") o.all_frames = true;
     else if (name == "StrictResolution") o.strict_res = true;
     else if (name == "BestModes") o.best_modes = val;
-    else if (name == "BatchFrames") o.batch = std::max(1, std::stoi(val));
+    else if (name == "BatchFrames") o.batch = val == "auto" ? 0 : std::max(1, std::stoi(val));
     else if (name == "Threads") o.threads = std::stoi(val);
     else if (name == "TopK") {
       o.topk = std::stoi(val);
@@ -490,7 +490,12 @@ int main(int argc, char **argv) {
   mip_opts_default(&opts);
   opts.filter = filter;
   opts.kernel_idx = o.kernel_idx;
-  opts.max_batch = std::min(o.batch, std::max(1, o.frames));
+  // Frames per device batch: each batch is one synchronous mip_search_frames call, whose
+  // pipeline fill and drain (first upload, last download) are paid per batch -- 8-frame
+  // batches searched 64 1080p frames in 23 ms, the search itself takes ~8.5 ms.  Auto: about
+  // 256 MB of samples per batch (32 frames at 1080p, 3 at 8K), bounding the pinned slots.
+  const int auto_batch = (int)std::max<long long>(1, std::min<long long>(32, (256LL << 20) / ((long long)W * H * 2)));
+  opts.max_batch = std::min(o.batch > 0 ? o.batch : auto_batch, std::max(1, o.frames));
   opts.want_sad_satd = o.sad_satd ? 1 : 0;
   opts.best_k = o.topk;
   std::vector<mip_engine *> engines;
