@@ -981,6 +981,24 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   ALLOC(e->d_queue, mipgpu::kQueueWords * 3 * mip_engine::kQueueSlots * sizeof(uint32_t));
   if (hipMemset(e->d_queue, 0, mipgpu::kQueueWords * 3 * mip_engine::kQueueSlots * sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail("hipMemset failed"));
+  // Every engine stream takes its hardware queue now, and the copy streams their copy
+  // engines (1 MiB each way through a page-locked buffer): HIP sets these up at their first
+  // use (tools/_r05ao.sh: the CLI's first download started 8-9 ms after the search it
+  // waited for).  (The counters are zero: rewriting one is harmless.)
+  {
+    void *h = nullptr;
+    const size_t nbytes = std::min<size_t>(1u << 20, fs * nb * 2);  // (d_frames' size)
+    bool ok = hipHostMalloc(&h, nbytes, hipHostMallocDefault) == hipSuccess;
+    for (hipStream_t st : {e->stream, e->stream4})
+      ok = ok && hipMemsetAsync(e->d_queue, 0, sizeof(uint32_t), st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(e->d_frames, h, nbytes, hipMemcpyHostToDevice, e->stream2) == hipSuccess &&
+         hipStreamSynchronize(e->stream2) == hipSuccess &&
+         hipMemcpyAsync(h, e->d_frames, nbytes, hipMemcpyDeviceToHost, e->stream3) == hipSuccess;
+    for (hipStream_t st : {e->stream, e->stream2, e->stream3, e->stream4})
+      ok = ok && hipStreamSynchronize(st) == hipSuccess;
+    if (h) (void)hipHostFree(h);
+    if (!ok) return cleanup(fail("initialising the engine streams failed"));
+  }
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   const size_t status_bytes = (size_t)(mip_engine::kCallRing + 1) * mipgpu::kStatusWords * sizeof(uint32_t);
