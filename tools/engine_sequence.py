@@ -67,6 +67,16 @@ if os.environ.get("RAW"):  # a plain 20 GB hipMalloc / hipFree in the engine's H
     print(json.dumps({"phase": "holding a 20 GB hipMalloc", "fps": rate()}), flush=True)
     assert hip.hipFree(p) == 0
     print(json.dumps({"phase": "after freeing it", "fps": rate()}), flush=True)
+    if os.environ.get("REFILL"):  # take the freed range again (held) before the next engine
+        q = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(q), ctypes.c_size_t(20 << 30)) == 0
+        print(json.dumps({"phase": "a second 20 GB allocation held", "fps": rate()}), flush=True)
+        assert hip.hipFree(q) == 0
+    for mb in (int(x) for x in os.environ.get("HOSTPIN_MB", "").split(",") if x):
+        b = pinned_empty((mb << 20,), np.uint8)
+        b[::4096] = 1
+        del b
+        print(json.dumps({"phase": "after %d MB page-locked host alloc + free" % mb, "fps": rate()}), flush=True)
 big_host()
 print(json.dumps({"phase": "after 6.8 GB page-locked host", "fps": rate()}), flush=True)
 big_engine()
