@@ -18,6 +18,7 @@
 
 #include "mip_kernels.h"
 #include "mip_tables.h"
+#include "chunk_plan.h"
 #include "host_stage_hip.h"
 #include "queue_ring.h"
 
@@ -1480,26 +1481,15 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // frame, under the next chunk's search; full tables are download-bound throughout, where a
   // ramp-down changes nothing).  The rest of the call keeps equal chunks of at most sb.
   // MIPGPU_RAMP=0 (A/B knob): no ramps; MIPGPU_RAMP=up: no ramp-down.
-  std::vector<int> plan, tail;
-  bool ramped = false;
+  int nhead = 0, ntail = 0;
+  std::vector<int> plan;
   {
-    int left = nframes;
     const char *rv = getenv("MIPGPU_RAMP");
     const bool ramps = nslots == 4 && sb >= 16 && !(rv && !strcmp(rv, "0"));
-    auto ramp = [&](std::vector<int> &v) {
-      for (int c = 4; c < sb && left > sb + c; c = c * 7 / 4) {
-        v.push_back(c);
-        left -= c;
-      }
-    };
-    if (ramps && idle && nframes >= 2 * sb) ramp(plan);
-    const bool head_empty = plan.empty();
-    if (ramps && sync && !down_per_frame && !(rv && !strcmp(rv, "up")) && left > sb) ramp(tail);
-    const int nch = (left + sb - 1) / sb, per = (left + nch - 1) / nch;
-    for (int f = 0; f < left; f += per) plan.push_back(std::min(per, left - f));
-    ramped = !tail.empty() || !head_empty;
-    plan.insert(plan.end(), tail.rbegin(), tail.rend());
+    plan = mipgpu::chunk_plan(nframes, sb, ramps && idle && nframes >= 2 * sb,
+                              ramps && sync && !down_per_frame && !(rv && !strcmp(rv, "up")), &nhead, &ntail);
   }
+  const bool ramped = nhead + ntail > 0;
   // Searches of consecutive chunks alternate between two search streams, so that a chunk's
   // search takes the CUs as its predecessor's persistent grid drains -- except in ramped
   // calls, whose short chunks are sized to run one after the other (device API, 1080p,
