@@ -59,6 +59,21 @@ int main() {
           CHECK(!(after_head > sb + ramp[h]), "n %d sb %d: head ramp stopped early at %d", n, sb, h);
         }
       }
+  // the call's chunk cap never exceeds a slot (an idle small engine's call of more
+  // than two slots' frames had been cut in halves larger than a slot)
+  for (int nslots = 3; nslots <= 4; nslots++)
+    for (int cap = 1; cap <= 64; cap++)
+      for (int n = 1; n <= 300; n++)
+        for (int idle = 0; idle < 2; idle++) {
+          const int sb = mipgpu::call_chunk_cap(n, cap, nslots, idle);
+          CHECK(sb >= 1 && sb <= cap, "n %d cap %d slots %d idle %d: chunk cap %d", n, cap, nslots, idle, sb);
+          if (nslots == 3 && idle && n >= 2)
+            CHECK(sb == std::min(cap, (n + 1) / 2), "n %d cap %d: idle split %d", n, cap, sb);
+          for (int c : mipgpu::chunk_plan(n, sb, false, false)) CHECK(c <= cap, "n %d cap %d: chunk %d", n, cap, c);
+        }
+  CHECK(mipgpu::call_chunk_cap(3, 1, 3, true) == 1, "max_batch 1, 3 frames");
+  CHECK(mipgpu::call_chunk_cap(9, 4, 3, true) == 4, "max_batch 4, 9 frames");
+  CHECK(mipgpu::call_chunk_cap(6, 4, 3, true) == 3, "max_batch 4, 6 frames");
   // the shapes documented in DESIGN.md section 6
   CHECK((mipgpu::chunk_plan(128, 64, true, false) == std::vector<int>{4, 7, 12, 21, 42, 42}), "128/64 head");
   CHECK((mipgpu::chunk_plan(128, 64, true, true) == std::vector<int>{4, 7, 12, 21, 37, 36, 7, 4}), "128/64 both");

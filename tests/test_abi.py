@@ -131,10 +131,14 @@ def test_wrong_result_knobs_are_refused_by_the_release_library(lib, monkeypatch,
 
 def test_one_hip_runtime_per_process():
     """Loading libmipgpu.so and then importing torch leaves ONE HIP runtime in the process
-    (torch's wheel bundles its own libamdhip64, loaded by path; mipgpu imports torch first so
-    the engine binds to it) -- two runtimes in one process made torch report no GPU once the
-    engine had opened it (round 5)."""
-    code = ("import sys; sys.path.insert(0, %r); import mipgpu; mipgpu.library(); import torch; "
-            "print(len(mipgpu.hip_runtimes()), mipgpu.hip_runtimes())" % os.path.join(REPO, "vvc-mip-gpu_amd"))
+    (torch's wheel bundles its own libamdhip64, loaded by path; mipgpu preloads that runtime by
+    path so the engine binds to it) -- two runtimes in one process made torch report no GPU
+    once the engine had opened it (round 5).  Loading the library does not import torch
+    (a multi-second import for numpy-only callers)."""
+    code = ("import sys; sys.path.insert(0, %r); import mipgpu; mipgpu.library(); "
+            "t = 'torch' in sys.modules; import torch; "
+            "print(len(mipgpu.hip_runtimes()), t, mipgpu.hip_runtimes())" % os.path.join(REPO, "vvc-mip-gpu_amd"))
     out = subprocess.check_output([sys.executable, "-c", code], text=True, timeout=300).strip()
-    assert out.startswith("1 "), out
+    assert out.startswith("1 False "), out
+    if mipgpu._torch_hip_runtime():
+        assert os.path.realpath(mipgpu._torch_hip_runtime()) in out, out

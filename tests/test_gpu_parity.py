@@ -775,3 +775,28 @@ def test_per_frame_pipeline_stress_1080p(gpu_available):
         assert np.array_equal(o["best_cost"][0], want["best_cost"][j]), (i, kind)
         if kind == "full":
             assert np.array_equal(o["cost"][0], want["cost"][j]), i
+
+
+@pytest.mark.parametrize("max_batch,n", [(1, 3), (1, 5), (4, 9), (4, 13)])
+def test_idle_call_chunks_fit_their_slot(gpu_available, max_batch, n):
+    """Small engines (max_batch < 16: three slots of max_batch frames) cut a call into an idle
+    pipeline in two -- but never into chunks larger than a slot (a call of more
+    than 2 x max_batch frames had spilled into the next slot's region).  Calls start at every
+    slot offset (0, 1 or 2 earlier one-frame chunks), so the first chunk lands in each slot,
+    incl. the last one; full tables + decisions, then decisions only; every frame equals the
+    oracle."""
+    w, h = 264, 136
+    frames = synth_frames(w, h, n, 0x1DC + 7 * max_batch + n, 0)
+    nct = layout.num_ctus(w, h)
+    want = [O.search(frames[f]) for f in range(n)]
+    for offset in range(3):
+        with MipEngine(w, h, max_batch=max_batch) as eng:
+            for i in range(offset):  # host_chunks = offset before the call under test
+                eng.search(frames[i:i + 1], costs=False, best=True)
+            full = eng.search(frames, best=True)
+            dec = eng.search(frames, costs=False, best=True)
+        for f in range(n):
+            bm, bc = layout.best_modes(want[f], nct)
+            assert np.array_equal(full["cost"][f], want[f]), (offset, f)
+            assert np.array_equal(full["best_mode"][f], bm), (offset, f)
+            assert np.array_equal(dec["best_mode"][f], bm) and np.array_equal(dec["best_cost"][f], bc), (offset, f)

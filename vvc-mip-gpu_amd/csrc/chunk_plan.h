@@ -6,6 +6,15 @@
 
 namespace mipgpu {
 
+// Largest chunk of a call before the transfer caps (mipgpu.cpp search_frames_chunks): a
+// slot's frames (`slot_cap`), or -- for a call into an idle pipeline on a small engine
+// (three slots) -- half the call, so that its own upload, search and download overlap, but
+// never more than a slot holds (a larger chunk would spill into the next slot's region).
+inline int call_chunk_cap(int nframes, int slot_cap, int nslots, bool idle) {
+  if (nslots == 3 && nframes >= 2 && idle) return std::min(slot_cap, (nframes + 1) / 2);
+  return slot_cap;
+}
+
 // nframes frames in chunks of at most sb.  `head`: the first chunks ramp up from 4 frames by
 // x1.75 (4, 7, 12, 21, ...) while more than sb frames stay for the rest; `tail`: the last
 // chunks ramp down the same way (..., 12, 7, 4), again leaving more than sb frames between;

@@ -749,16 +749,14 @@ static uint32_t *call_status(mip_engine *e, uint64_t call) {
 }
 
 // Host API: move the status sets of the completed calls (status_harvested, upto] into
-// call_errors (only calls that saw a violation are kept; at most kMaxCallErrors of them).
-// Every call <= upto must have completed.
+// call_errors (only calls that saw a violation are kept, until mip_wait reports them: an
+// entry is never dropped, so a call that searched samples above 1023 can never be waited for
+// as a success; memory is bounded by the failed calls nobody waits for -- the Python
+// binding's tickets wait when dropped).  Every call <= upto must have completed.
 static void harvest_status(mip_engine *e, uint64_t upto) {
-  constexpr size_t kMaxCallErrors = 4096;
   for (uint64_t c = e->status_harvested + 1; c <= upto; c++) {
     const uint32_t f = take_status(e, (int)((c - 1) % mip_engine::kCallRing));
-    if (f) {
-      if (e->call_errors.size() >= kMaxCallErrors) e->call_errors.erase(e->call_errors.begin());
-      e->call_errors[c] = f;
-    }
+    if (f) e->call_errors[c] = f;
   }
   if (upto > e->status_harvested) e->status_harvested = upto;
 }
@@ -1410,13 +1408,13 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // between calls -- outputs requested, call length -- but a slot's region never moves, so
   // the per-slot events order every reuse of it)
   const int slot_cap = e->hp_cap;
-  int sb = slot_cap;
-  // A call into an idle pipeline (nothing queued before it) is cut in two, so that its own
-  // upload, search and download overlap; calls queued behind others keep whole-call chunks
-  // (the overlap comes from the neighbouring calls, and larger launches are more efficient).
+  // A call into an idle pipeline (nothing queued before it) is cut in two (at most a slot's
+  // frames each), so that its own upload, search and download overlap; calls queued behind
+  // others keep whole-slot chunks (the overlap comes from the neighbouring calls, and larger
+  // launches are more efficient).  sb only shrinks below.
   const bool idle = e->host_calls == 0 ||
                     hipEventQuery(e->call_done[(e->host_calls - 1) % mip_engine::kCallRing]) == hipSuccess;
-  if (nslots == 3 && nframes >= 2 && idle) sb = (nframes + 1) / 2;
+  int sb = mipgpu::call_chunk_cap(nframes, slot_cap, nslots, idle);
   // Full tables to the host (PCIe-bound): chunks of at most ~1 GiB of downloads, so the
   // first download starts early and, for pageable outputs, the bounce ring's copy-out keeps
   // up (1080p, 8 calls of 128 frames: 96-frame chunks 831 frames/s pageable, 32-frame 892,
@@ -1497,6 +1495,8 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // two streams; host pipeline: 8 queued one-frame calls decisions-only +5 %, 4-frame +4 %,
   // one synchronous ramped 128-frame call -2 %, so ramped calls keep one stream).
   const bool alt_streams = search_streams() == 2 && !ramped;
+  for (const int nb : plan)  // (chunk_plan never exceeds sb <= slot_cap: a slot's region)
+    if (nb < 1 || nb > slot_cap) return fail("internal: a chunk of %d frames for a slot of %d", nb, slot_cap);
   int f0 = 0;
   for (const int nb : plan) {
     const uint64_t k = e->host_chunks++;

@@ -62,17 +62,32 @@ class _Opts(ctypes.Structure):
 _lib = None
 
 
+def _torch_hip_runtime():
+    """Path of the HIP runtime bundled in torch's ROCm wheel (torch/lib/libamdhip64.so), or None
+    when torch is not installed or bundles none -- found without importing torch."""
+    spec = importlib.util.find_spec("torch")
+    for d in (spec.submodule_search_locations or []) if spec is not None else []:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            return p
+    return None
+
+
 def _one_hip_runtime():
     """One HIP runtime per process.  torch's ROCm wheel bundles its own libamdhip64 /
-    libhsa-runtime64 and loads them by path, so if libmipgpu.so were loaded first (binding
-    /opt/rocm's runtime) a later `import torch` would bring a second HIP and HSA runtime into
-    the process, and torch then finds no GPU once ours has opened it.  When torch is
-    installed it is imported first, and libmipgpu.so binds to the runtime torch loaded (same
-    soname).  MIPGPU_NO_TORCH=1 skips this (a process that never imports torch)."""
+    libhsa-runtime64 and loads them by path, so if libmipgpu.so bound /opt/rocm's runtime a
+    later `import torch` would bring a second HIP and HSA runtime into the process, and torch
+    then finds no GPU once ours has opened it.  So when torch is installed, its bundled
+    runtime is loaded first -- by path, with RTLD_GLOBAL, without importing torch (a
+    multi-second import with process-wide side effects that numpy-only callers and the CLI
+    wrappers do not need) -- and libmipgpu.so binds to it (same soname, libamdhip64.so.7); a
+    later `import torch` finds it already mapped.  MIPGPU_NO_TORCH=1 skips this (a process
+    that never imports torch: /opt/rocm's runtime)."""
     if "torch" in sys.modules or os.environ.get("MIPGPU_NO_TORCH"):
         return
-    if importlib.util.find_spec("torch") is not None:
-        import torch  # noqa: F401
+    path = _torch_hip_runtime()
+    if path is not None:
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 
 def hip_runtimes():
