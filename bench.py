@@ -62,6 +62,7 @@ DUAL_CEILINGS = {"all_dual_eligible": 1.37, "none_dual_eligible": 0.86, "unit": 
 VECTOR_OPS_PER_CTU = 99.6e6
 E2E_CALLS = 8  # host-buffer calls queued per end-to-end measurement round
 E2E_ROUNDS = 3  # timed rounds per end-to-end leg (median reported)
+E2E_FRAMES_MULTI = 32  # frames per host-buffer call at N > 1 (bounds each rank's page-locked memory)
 
 
 def metric_name(width, height):
@@ -374,6 +375,39 @@ def ranks_section(per_rank, frames_per_step, steps, backend, devices=None):
             "per_rank_kernel_ms": [round(r[1], 4) for r in per_rank]}
 
 
+def timed_rounds(run_round, world, coll_dev, frames_per_round, rounds=E2E_ROUNDS):
+    """End-to-end leg over all ranks: one warm-up round, then `rounds` timed rounds, each
+    aligned by a barrier (N > 1) and timed by its slowest rank (max over ranks).  Returns the
+    median whole-job rate (all ranks' frames / the slowest rank's time), every round's rate,
+    and this rank's own median rate (its frames / its own time)."""
+    import statistics
+    agg, own = [], []
+    for r in range(1 + rounds):
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        t0 = time.perf_counter()
+        run_round()
+        dt = time.perf_counter() - t0
+        slowest = dist_max(dt, world, coll_dev)
+        if r:
+            agg.append(world * frames_per_round / slowest)
+            own.append(frames_per_round / dt)
+    return round(statistics.median(agg), 2), [round(x, 1) for x in agg], round(statistics.median(own), 2)
+
+
+def e2e_multi_section(legs, world, coll_dev, frames_per_call, note):
+    """`end_to_end` at N > 1: each leg's whole-job rate (`aggregate`) and every rank's own rate
+    (`ranks`), gathered on every rank (collective), for rank 0 to print."""
+    res = {"unit": "frames/s", "world_size": world, "frames_per_call": frames_per_call, "calls_per_round": E2E_CALLS,
+           "aggregate": {}, "rounds": {}, "ranks": {}, "note": note}
+    for name, (value, rounds, own) in legs.items():
+        res["aggregate"][name] = value
+        res["rounds"][name] = rounds
+        res["ranks"][name] = [round(r[0], 2) for r in gather_ranks([own], world, coll_dev)]
+    return res
+
+
 def plumbing_check(args):
     """--plumbing-check: the multi-rank path of main() on CPU (gloo), a sleep per step."""
     import torch.distributed as dist
@@ -391,12 +425,21 @@ def plumbing_check(args):
     per_rank = gather_ranks([elapsed, 1e3 * own / args.steps], world)
     max_elapsed = max(r[0] for r in per_rank)
     value, ms_per_step = aggregate(args.frames_per_step, args.steps, world, max_elapsed)
+    # the end-to-end legs' aggregation at N > 1 (a sleep per round; rank r the (r+1)-times slower)
+    e2e = None
+    if world > 1 and not args.no_end_to_end:
+        legs = {"value": timed_rounds(lambda: time.sleep(0.01 * (1 + rank)), world, None, E2E_CALLS * E2E_FRAMES_MULTI),
+                "decisions_value": timed_rounds(lambda: time.sleep(0.005 * (1 + rank)), world, None,
+                                                E2E_CALLS * E2E_FRAMES_MULTI)}
+        e2e = e2e_multi_section(legs, world, None, E2E_FRAMES_MULTI, "plumbing check (sleep per round)")
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
-                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-                          "data": "plumbing check (no GPU, sleep per step)",
-                          "ranks": ranks_section(per_rank, args.frames_per_step, args.steps,
-                                                 "gloo" if world > 1 else None)}), flush=True)
+        line = {"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+                "data": "plumbing check (no GPU, sleep per step)",
+                "ranks": ranks_section(per_rank, args.frames_per_step, args.steps, "gloo" if world > 1 else None)}
+        if e2e:
+            line["end_to_end"] = e2e
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -455,6 +498,10 @@ def main():
     backend, dev_index, coll_dev = init_ranks(world, local_rank, ndev)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
+    # the rank's host side on its GPU's NUMA node (mip_bind_thread; no-op on a one-node host):
+    # its page-locked buffers (pinned_empty(device=...)) and the engine's threads are placed too
+    from mipgpu import bind_thread, numa_node
+    numa = {"node": numa_node(dev_index), "thread_bound": bind_thread(dev_index)}
     W, H, B = args.width, args.height, args.frames_per_step
 
     # synthetic frames generated on the GPU (bit-identical to mipgpu.synth.synth_frames)
@@ -488,6 +535,34 @@ def main():
     max_kernel_ms = max(r[1] for r in per_rank)
     value, ms_per_step = aggregate(B, args.steps, world, max_elapsed)
 
+    e2e_multi = None
+    if world > 1 and not args.no_end_to_end:
+        # Host-fed rate of the whole job (informative, never `value`): every rank feeds its own
+        # GPU from page-locked host buffers on that GPU's NUMA node -- E2E_CALLS asynchronous
+        # calls of E2E_FRAMES_MULTI frames per round, rounds aligned by a barrier and timed by
+        # the slowest rank.  Full int32 cost tables (52.8 MB per 1080p frame over PCIe) and
+        # decisions only.
+        from mipgpu import pinned_empty
+        Bm = min(B, E2E_FRAMES_MULTI)
+        hp = pinned_empty((Bm, H, W), np.uint16, device=dev_index)
+        hp[:] = frames[:Bm].cpu().numpy().view(np.uint16)
+        cost_out = {"cost": pinned_empty((Bm, eng.costs_per_frame), np.int32, device=dev_index)}
+        dec_out = {"best_mode": pinned_empty((Bm, eng.cus_per_frame), np.uint8, device=dev_index),
+                   "best_cost": pinned_empty((Bm, eng.cus_per_frame), np.int32, device=dev_index)}
+
+        def leg(**kw):
+            return timed_rounds(lambda: eng.wait([eng.search_async(hp, **kw) for _ in range(E2E_CALLS)][-1]),
+                                world, coll_dev, E2E_CALLS * Bm)
+        legs = {"value": leg(out=cost_out), "decisions_value": leg(costs=False, best=True, out=dec_out)}
+        e2e_multi = e2e_multi_section(
+            legs, world, coll_dev, Bm,
+            "host frames in (page-locked, on the rank's GPU's NUMA node), per rank %d asynchronous calls of %d "
+            "frames per round, rounds aligned by a barrier; aggregate = all ranks' frames / the slowest rank's "
+            "time (median of %d rounds after a warm-up round); value: int32 cost tables out (%.1f MB per frame), "
+            "decisions_value: per-CU best mode + cost out" % (E2E_CALLS, Bm, E2E_ROUNDS,
+                                                              algorithmic_bytes_per_frame(W, H) / 1e6))
+        del hp, cost_out, dec_out
+
     cfg = {(1920, 1080, None): 1, (1920, 1080, "filterFrame_2d_float_5x5_quarterCtu"): 2, (3840, 2160, None): 3,
            (7680, 4320, "filterFrame_2d_int_quarterCtu"): 4}.get((W, H, args.refs_filter))
     refs_desc = ("original references" if args.refs_filter is None else
@@ -518,8 +593,17 @@ def main():
             "valu": valu_section(pmc, max_kernel_ms, ops),
             "ranks": ranks_section(per_rank, B, args.steps, backend if world > 1 else None,
                                    devices=ndev),
-            "build_id": build, "pmc_source": pmc_src,
+            "build_id": build, "pmc_source": pmc_src, "numa": numa,
         }
+        if e2e_multi is not None:
+            res["end_to_end"] = e2e_multi
+        if world > max(1, ndev):  # a rehearsal: ranks time-share GPUs
+            note = ("%d ranks share %d GPU(s): each kernel time is a time-shared one, so the roofline / VALU fields "
+                    "are not meaningful here (the rank bookkeeping and aggregation are what this line checks)"
+                    % (world, ndev))
+            for key in ("roofline", "valu"):
+                res[key]["meaningful"] = False
+                res[key]["note"] = note
         if knobs:
             res["knobs"] = knobs
             res["headline"] = False  # measured with work knobs set (A/B tooling)
@@ -567,7 +651,7 @@ def main():
             from mipgpu import pinned_empty
             Be = min(B, 128)  # frames per call (bounded host memory: 6.8 GB of int32 costs per call)
             host = frames[:Be].cpu().numpy().view(np.uint16)
-            hp = pinned_empty(host.shape, np.uint16)
+            hp = pinned_empty(host.shape, np.uint16, device=dev_index)
             hp[:] = host
 
             def e2e_leg(fr, **kw):
@@ -579,7 +663,8 @@ def main():
                         rates.append(E2E_CALLS * Be / (time.perf_counter() - t0))
                 return round(statistics.median(rates), 2), [round(x, 1) for x in rates]
 
-            pinned_fps, pinned_all = e2e_leg(hp, out={"cost": pinned_empty((Be, eng.costs_per_frame), np.int32)})
+            pinned_fps, pinned_all = e2e_leg(hp, out={"cost": pinned_empty((Be, eng.costs_per_frame), np.int32,
+                                                                           device=dev_index)})
             # pageable (malloc'd) buffers, staged through the engine's page-locked bounce ring:
             # steady state with outputs the caller reuses (touched, like pinned ones above) and
             # a cold call into a fresh allocation (first-touch page faults of 6.8 GB included)
@@ -591,8 +676,8 @@ def main():
             eng.search(host)
             pageable_cold_fps = Be / (time.perf_counter() - t0)
             # decisions only: frames in, per-CU best mode + cost out (no cost table: fused argmin)
-            dout = {"best_mode": pinned_empty((Be, eng.cus_per_frame), np.uint8),
-                    "best_cost": pinned_empty((Be, eng.cus_per_frame), np.int32)}
+            dout = {"best_mode": pinned_empty((Be, eng.cus_per_frame), np.uint8, device=dev_index),
+                    "best_cost": pinned_empty((Be, eng.cus_per_frame), np.int32, device=dev_index)}
             decisions_fps, decisions_all = e2e_leg(hp, costs=False, best=True, out=dout)
             res["end_to_end"] = {"value": pinned_fps, "unit": "frames/s",
                                  "pageable_value": pageable_fps,

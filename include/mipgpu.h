@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MIPGPU_ABI_VERSION 6
+#define MIPGPU_ABI_VERSION 7
 #define MIP_COSTS_PER_CTU_ABI 97840
 #define MIP_CUS_PER_CTU_ABI 5380
 #define MIP_COST_UNAVAILABLE 0x7fffffff
@@ -140,7 +140,14 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
  * still in flight (the upload / search / download pipeline stays full from one call to the
  * next) and returns a ticket (> 0) in *ticket.  The host buffers must stay valid and
  * unmodified (inputs) / unread (outputs) until mip_wait(e, ticket) returns.  Calls complete
- * in order.  mip_filter_frames waits for every call in flight. */
+ * in order.  mip_filter_frames waits for every call in flight.
+ * Merged launches (ABI 7): a call with page-locked buffers and fewer frames than one buffer
+ * slot (opts.max_batch below 16, else max_batch / 4) that arrives while the pipeline is busy
+ * joins the engine's open chunk -- calls with the same outputs and reference source share ONE
+ * search launch (one-frame calls then run at the multi-frame launch rate).  The chunk is
+ * launched when full, when an incompatible call arrives, at any mip_wait / synchronous call /
+ * device-API call of the engine, or by the engine's own thread as soon as the search before it
+ * has completed.  Every call keeps its own ticket, outputs and input-contract status. */
 int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
                             int nframes, int32_t *costs_out, uint8_t *best_mode_out,
                             int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out,
@@ -214,12 +221,30 @@ double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uin
 int mip_trace_times(mip_engine *e, int enable);
 int mip_pop_times(mip_engine *e, double *upload_ms, double *filter_ms, int max, int *n);
 
+/* Host-pipeline counters of the engine (diagnostics, tests): out[0] host-API calls, out[1]
+ * search launches of the host pipeline (chunks), out[2] calls that went through merged
+ * chunks, out[3] merged launches (n entries of out are written, n <= 4). */
+int mip_host_stats(mip_engine *e, uint64_t *out, int n);
+
 /* Page-locked host memory (hipHostMalloc): host buffers for mip_search_frames /
  * mip_filter_frames allocated here are transferred by DMA at full PCIe rate (pageable
  * buffers are staged through the runtime -- the cost table is 52.8 MB per 1080p frame).
  * Replaces the reference's malloc'd return_minSadHad etc. (main.cpp:656-668). */
 int mip_host_alloc(size_t bytes, void **out);
 int mip_host_free(void *p);
+
+/* NUMA placement (ABI 7).  Each GPU hangs off one socket of a multi-socket host; an engine
+ * keeps its page-locked buffers on that GPU's NUMA node and runs its host threads (bounce-ring
+ * copies, completion, merge flusher) on the node's CPUs.  mip_host_alloc_near allocates the
+ * caller's page-locked buffers on `device`'s node (else as mip_host_alloc);
+ * mip_bind_thread runs the calling thread on the node's CPUs (1 bound, 0 nothing to do: one
+ * node or unknown); mip_numa_node gives the node (-1 unknown / one node);
+ * mip_numa_node_of_pci the node of a PCI bus id ("0000:c1:00.0"), read from sysfs
+ * (MIPGPU_SYSFS_ROOT overrides /sys). */
+int mip_host_alloc_near(int device, size_t bytes, void **out);
+int mip_bind_thread(int device);
+int mip_numa_node(int device);
+int mip_numa_node_of_pci(const char *pci_bus_id);
 
 /* Last error message of the calling thread ("" if none). */
 const char *mip_last_error(void);

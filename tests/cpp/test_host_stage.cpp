@@ -80,7 +80,7 @@ struct SimDev {
   static constexpr Err kNotReady = 3;
   Sim *sim;
   std::atomic<int> *allocs;
-  Err host_alloc(char **p, size_t n) {
+  Err host_alloc(char **p, size_t n, bool) {
     *p = new char[n];
     allocs->fetch_add(1);
     return kOk;

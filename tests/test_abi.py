@@ -39,7 +39,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_geometry_helpers(lib):
-    assert lib.mip_abi_version() == 6
+    assert lib.mip_abi_version() == 7
     assert lib.mip_num_ctus(1920, 1080) == 135
     assert lib.mip_num_ctus(3840, 2160) == 510
     assert lib.mip_num_ctus(7680, 4320) == 2040

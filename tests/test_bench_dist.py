@@ -72,6 +72,16 @@ def test_gpus_flag_without_launcher_starts_ranks():
     # barriers), so at most twice the slow rank's own rate
     assert abs(line["value"] - 2 * 5 * 4 / (5 * line["ms_per_step"] * 1e-3)) / line["value"] < 1e-3
     assert line["value"] <= 2 * per[1] * 1.001
+    # the end-to-end legs at N > 1: every rank runs them, aggregate = all ranks' frames over the
+    # slowest rank's time per round (rank 1 sleeps 20 ms / 10 ms per round), each rank's own rate
+    e2e = line["end_to_end"]
+    assert e2e["world_size"] == 2 and e2e["frames_per_call"] == bench.E2E_FRAMES_MULTI
+    frames = 2 * bench.E2E_CALLS * bench.E2E_FRAMES_MULTI
+    for leg, slow_s in (("value", 0.02), ("decisions_value", 0.01)):
+        assert 0.5 * frames / slow_s < e2e["aggregate"][leg] <= frames / slow_s, (leg, e2e)
+        own = e2e["ranks"][leg]
+        assert len(own) == 2 and own[0] > own[1], (leg, own)
+        assert len(e2e["rounds"][leg]) == bench.E2E_ROUNDS
 
 
 def test_gpus_flag_must_match_launcher():

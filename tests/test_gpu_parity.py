@@ -800,3 +800,114 @@ def test_idle_call_chunks_fit_their_slot(gpu_available, max_batch, n):
             assert np.array_equal(full["cost"][f], want[f]), (offset, f)
             assert np.array_equal(full["best_mode"][f], bm), (offset, f)
             assert np.array_equal(dec["best_mode"][f], bm) and np.array_equal(dec["best_cost"][f], bc), (offset, f)
+
+
+@pytest.mark.parametrize("filt,k", [(None, 0), ("filterFrame_2d_float_5x5_quarterCtu", 2)])
+def test_merged_launches_keep_each_call_its_own(gpu_available, monkeypatch, filt, k):
+    """Merged launches (mipgpu.cpp open chunk, ABI 7): small page-locked calls share one search
+    launch.  MIPGPU_MERGE=hold makes the grouping deterministic (chunks open even into an idle
+    pipeline and are launched only by the other triggers): four decisions-only calls, three
+    full-table calls, caller references (1 + 2 frames), then four decisions-only calls of which
+    one holds a sample above 1023, then an 8-frame call (a whole slot: not merged).  Every call
+    equals the oracle, the bad call -- and only it -- fails at its own wait, and the counters
+    show exactly four merged launches of 13 calls."""
+    from mipgpu import pinned_empty
+    monkeypatch.setenv("MIPGPU_MERGE", "hold")
+    w, h = 264, 136
+    n = 23
+    frames = synth_frames(w, h, n, 0x3E6 + (k or 0), 0)
+    refs = synth_frames(w, h, 3, 0x3E7, 0)
+    bad = 14  # frame of the bad call
+    pf = pinned_empty(frames.shape, np.uint16)
+    pf[:] = frames
+    pf[bad, 40, 77] = 1024
+    pr = pinned_empty(refs.shape, np.uint16)
+    pr[:] = refs
+    nct = layout.num_ctus(w, h)
+
+    def outs(nf, full):
+        o = {"best_mode": pinned_empty((nf, nct * layout.CUS_PER_CTU), np.uint8),
+             "best_cost": pinned_empty((nf, nct * layout.CUS_PER_CTU), np.int32)}
+        if full:
+            o["cost"] = pinned_empty((nf, nct * layout.COSTS_PER_CTU), np.int32)
+        return o
+    # (first frame, frames, kind): dec / full / refs (full table, caller references)
+    calls = [(0, 1, "dec"), (1, 1, "dec"), (2, 1, "dec"), (3, 1, "dec"),
+             (4, 1, "full"), (5, 1, "full"), (6, 1, "full"),
+             (7, 1, "refs"), (8, 2, "refs"),
+             (12, 1, "dec"), (bad, 1, "dec"), (13, 1, "dec"), (10, 1, "dec"),
+             (15, 8, "dec")]
+    with MipEngine(w, h, max_batch=8, filter=filt, kernel_idx=k) as eng:
+        tickets = []
+        for f0, nf, kind in calls:
+            r = pr[f0 - 7:f0 - 7 + nf] if kind == "refs" else None
+            tickets.append(eng.search_async(pf[f0:f0 + nf], refs=r, costs=kind != "dec", best=True,
+                                            out=outs(nf, kind != "dec")))
+        results = []
+        for t in tickets:
+            try:
+                results.append(eng.wait(t))
+            except MipError as exc:
+                results.append(exc)
+        stats = eng.host_stats()
+    assert stats["merged_launches"] == 4 and stats["merged_calls"] == 13, stats
+    assert stats["calls"] == len(calls) and stats["launches"] >= 5, stats
+    for (f0, nf, kind), res in zip(calls, results):
+        if f0 == bad:
+            assert isinstance(res, MipError) and "above 10 bits" in str(res), res
+            continue
+        assert not isinstance(res, MipError), (f0, kind, res)
+        for i in range(nf):
+            f = f0 + i
+            if kind == "refs":
+                oc = O.search(frames[f], refs[f - 7])
+            else:
+                oc = O.engine_search(frames[f], filt, k)
+            bm, bc = layout.best_modes(oc, nct)
+            assert np.array_equal(res["best_mode"][i], bm), (f0, kind, i)
+            assert np.array_equal(res["best_cost"][i], bc), (f0, kind, i)
+            if kind != "dec":
+                assert np.array_equal(res["cost"][i], oc), (f0, kind, i)
+
+
+def test_merged_launches_1080p_default_policy(gpu_available):
+    """Default merge policy at the bench size: 24 one-frame 1080p calls queued back to back
+    (page-locked, decisions only and full tables in runs) merge while the pipeline is busy;
+    every output equals a synchronous search of the same frame.  Then the flusher thread: a
+    one-frame call queued behind a 4-frame call is launched without any wait (the counters
+    show its merged launch after the 4-frame search has completed)."""
+    import time
+    from mipgpu import pinned_empty
+    W, H = 1920, 1080
+    pool = synth_frames(W, H, 4, 0x6E7, 0)
+    with MipEngine(W, H, max_batch=4) as ref_eng:
+        want = ref_eng.search(pool, best=True)
+    with MipEngine(W, H, max_batch=8) as eng:
+        pf = pinned_empty(pool.shape, np.uint16)
+        pf[:] = pool
+        tickets, kinds = [], []
+        for i in range(24):
+            full = (i // 6) % 2 == 1
+            out = {"best_mode": pinned_empty((1, eng.cus_per_frame), np.uint8),
+                   "best_cost": pinned_empty((1, eng.cus_per_frame), np.int32)}
+            if full:
+                out["cost"] = pinned_empty((1, eng.costs_per_frame), np.int32)
+            tickets.append(eng.search_async(pf[i % 4:i % 4 + 1], costs=full, best=True, out=out))
+            kinds.append(full)
+        outs = [eng.wait(t) for t in tickets]
+        s0 = eng.host_stats()
+        assert s0["merged_calls"] >= 1, s0
+        for i, (full, o) in enumerate(zip(kinds, outs)):
+            j = i % 4
+            assert np.array_equal(o["best_mode"][0], want["best_mode"][j]), (i, full)
+            assert np.array_equal(o["best_cost"][0], want["best_cost"][j]), (i, full)
+            if full:
+                assert np.array_equal(o["cost"][0], want["cost"][j]), i
+        # the flusher thread
+        t4 = eng.search_async(pf, costs=False, best=True)   # 4 frames of a 8-frame slot: launched
+        t1 = eng.search_async(pf[2:3], costs=False, best=True)  # busy: opens a chunk
+        time.sleep(0.5)
+        s1 = eng.host_stats()
+        assert s1["merged_launches"] == s0["merged_launches"] + 1, (s0, s1)
+        o4, o1 = eng.wait(t4), eng.wait(t1)
+        assert np.array_equal(o4["best_mode"], want["best_mode"]) and np.array_equal(o1["best_cost"][0], want["best_cost"][2])

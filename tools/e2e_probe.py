@@ -114,10 +114,11 @@ def run(case, W, H, calls, reps, torch_after=None, device_first=0, sync=False):
             enq.append(1e3 * (t1 - t0))
             wt.append(1e3 * (t2 - t1))
             del tickets
+        stats = eng.host_stats() if hasattr(eng, "host_stats") else None
     return {"case": case, "hip_runtime": hip_runtimes(), "frames_per_call": F, "out": out, "host": host, "filter": flt, "kernel_idx": kidx,
             "max_batch": mb, "calls": calls, "sync": sync, "fps": round(float(np.median(rates)), 1),
             "fps_all": [round(r, 1) for r in rates], "enqueue_ms": [round(x, 3) for x in enq],
-            "wait_ms": [round(x, 3) for x in wt]}
+            "wait_ms": [round(x, 3) for x in wt], "host_stats": stats}
 
 
 def main():

@@ -7,10 +7,12 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out}/multirank
 mkdir -p "$OUT"
-ARGS="--frames-per-step 128 --steps 10 --warmup 2 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter --no-end-to-end"
+# (round 6: the end-to-end legs run on every rank at N > 1 -- end_to_end.aggregate)
+ARGS="--frames-per-step 128 --steps 10 --warmup 2 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter"
+ARGS1="$ARGS --no-end-to-end"
 # the driver's 8-GPU launch shape, rehearsed with 8 ranks on this box's one device (round 5:
 # launcher, rendezvous, `ranks`, max over 8 ranks; 32 frames per rank keep 8 engines in HBM)
-ARGS8="--frames-per-step 32 --steps 10 --warmup 2 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter --no-end-to-end"
+ARGS8="--frames-per-step 32 --steps 10 --warmup 2 --no-cpu-baseline --no-reference-gpu --no-latency --no-filter"
 echo "== bench --gpus 8 (own ranks, 8 ranks sharing device 0) $(date +%T)"
 timeout -k 10 400 python bench.py --gpus 8 $ARGS8 > "$OUT/bench_gpus8.json" 2> "$OUT/bench_gpus8.err" || { tail -20 "$OUT/bench_gpus8.err"; exit 1; }
 cat "$OUT/bench_gpus8.json"
@@ -26,7 +28,7 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   --master-port 29531 bench.py --gpus 2 $ARGS > "$OUT/bench_torchrun2.json" 2> "$OUT/bench_torchrun2.err" || { tail -20 "$OUT/bench_torchrun2.err"; exit 1; }
 cat "$OUT/bench_torchrun2.json"
 echo "== bench --gpus 1 (same box, reference) $(date +%T)"
-timeout -k 10 300 python bench.py $ARGS > "$OUT/bench_gpus1.json" 2> "$OUT/bench_gpus1.err" || { tail -20 "$OUT/bench_gpus1.err"; exit 1; }
+timeout -k 10 300 python bench.py $ARGS1 > "$OUT/bench_gpus1.json" 2> "$OUT/bench_gpus1.err" || { tail -20 "$OUT/bench_gpus1.err"; exit 1; }
 cat "$OUT/bench_gpus1.json"
 echo "== CLI --DeviceIndex 0,0, 2 frames $(date +%T)"
 python3 - <<'PY'

@@ -191,14 +191,16 @@ int report_parameters(const Options &o, bool alt) {
   return errors;
 }
 
-// Page-locked host buffer (mip_host_alloc): the engine's transfers run at DMA rate.
+// Page-locked host buffer (mip_host_alloc): the engine's transfers run at DMA rate.  With one
+// device, on that GPU's NUMA node (mip_host_alloc_near).
 template <class T>
 struct Pinned {
   T *p = nullptr;
   size_t n = 0;
-  bool alloc(size_t count) {
+  bool alloc(size_t count, int near_device = -1) {
     void *v = nullptr;
-    if (mip_host_alloc(count * sizeof(T), &v) != 0) return false;
+    if ((near_device >= 0 ? mip_host_alloc_near(near_device, count * sizeof(T), &v) : mip_host_alloc(count * sizeof(T), &v)) != 0)
+      return false;
     p = static_cast<T *>(v);
     n = count;
     return true;
@@ -570,11 +572,13 @@ int main(int argc, char **argv) {
   std::vector<Slot> slots(kSlots);
   const bool cost_all = want_bin || o.all_frames;
   bool ok = true;
+  const int near = ndev == 1 ? o.devices[0] : -1;  // (a slot's frames are shared by every device's shard)
   for (Slot &sl : slots) {
     const size_t n = (size_t)std::min(chunk, std::max(1, o.frames));
-    ok = ok && sl.in.alloc(n * fs) && sl.cost.alloc((cost_all ? n : 1) * cpf);
-    if (o.sad_satd) ok = ok && sl.sad.alloc((cost_all ? n : 1) * cpf) && sl.satd.alloc((cost_all ? n : 1) * cpf);
-    if (want_best) ok = ok && sl.best.alloc(n * upf) && sl.best_cost.alloc(n * upf);
+    ok = ok && sl.in.alloc(n * fs, near) && sl.cost.alloc((cost_all ? n : 1) * cpf, near);
+    if (o.sad_satd)
+      ok = ok && sl.sad.alloc((cost_all ? n : 1) * cpf, near) && sl.satd.alloc((cost_all ? n : 1) * cpf, near);
+    if (want_best) ok = ok && sl.best.alloc(n * upf, near) && sl.best_cost.alloc(n * upf, near);
   }
   if (!ok) {
     std::cout << "  [!] ERROR: " << mip_last_error() << std::endl;
@@ -667,6 +671,7 @@ int main(int argc, char **argv) {
       const size_t co = cost_all ? a * cpf : 0;
       const int nb = cost_all || !dc ? b - a : 1;
       workers.emplace_back([&, d, a, b, dc, co, nb] {
+        (void)mip_bind_thread(o.devices[d]);  // the device's host thread on its GPU's NUMA node
         rcs[d] = 0;
         if (!dc || nb == b - a)
           rcs[d] = mip_search_frames(engines[d], sl.in.data() + a * fs, nullptr, b - a, dc ? sl.cost.data() + co : nullptr,

@@ -8,7 +8,8 @@
 // rounds, tools/e2e_probe.py enqueue_ms, round 5).  The claim word carries the job's
 // generation, so a worker that wakes up after its job has ended (or while a later one runs)
 // claims nothing of a job whose parameters it did not read.  No HIP dependency
-// (tests/cpp/test_copy_pool.cpp).
+// (tests/cpp/test_copy_pool.cpp).  The workers run on the CPUs of the engine's NUMA place
+// when one is given (numa_place.h).
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -19,6 +20,8 @@
 #include <thread>
 #include <vector>
 
+#include "numa_place.h"
+
 namespace mipgpu {
 
 class CopyPool {
@@ -26,8 +29,12 @@ class CopyPool {
   static constexpr size_t kChunk = 1u << 20;
   static constexpr size_t kMinParallel = 4u << 20;  // smaller copies: one memcpy on the caller
 
-  explicit CopyPool(int n) {
-    for (int i = 0; i < n; i++) th_.emplace_back([this] { run(); });
+  explicit CopyPool(int n, const NumaPlace &place = NumaPlace()) {
+    for (int i = 0; i < n; i++)
+      th_.emplace_back([this, place] {
+        (void)bind_current_thread(place);
+        run();
+      });
   }
   ~CopyPool() {
     {

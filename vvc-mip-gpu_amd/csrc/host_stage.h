@@ -43,7 +43,9 @@ namespace mipgpu {
 
 // Dev provides: types Err, Stream, Event; static constexpr Err kOk, kNotReady (a transfer
 // before reserve()); and
-//   Err host_alloc(char **p, size_t n);        void host_free(char *p);
+//   Err host_alloc(char **p, size_t n, bool numa_user);   void host_free(char *p);
+//                                             (numa_user: the pages follow the calling
+//                                             thread's memory policy, numa_place.h)
 //   Err event_create(Event *e);                void event_destroy(Event e);
 //   Err copy_h2d(void *dev, const void *host, size_t n, Stream s);
 //   Err copy_d2h(void *host, const void *dev, size_t n, Stream s);
@@ -92,6 +94,9 @@ class BounceRing {
     release();
   }
   void set_device(int device) { device_ = device; }
+  // NUMA placement of the ring (numa_place.h): the arena's pages, the copy pool's and the
+  // completion thread's CPUs.  Before the first reserve().
+  void set_place(const NumaPlace &p) { place_ = p; }
 
   // Allocate the ring (kRing pieces of `piece` bytes) if it is not there or smaller.
   Err reserve(size_t piece) {
@@ -104,7 +109,11 @@ class BounceRing {
     Err e = drain(~0ull);
     if (e != Dev::kOk) return e;
     release();
-    if ((e = dev_.host_alloc(&arena_, piece * kRing)) != Dev::kOk) {
+    {
+      const ScopedNodePolicy pol(place_);  // (the arena's pages on the GPU's node)
+      e = dev_.host_alloc(&arena_, piece * kRing, pol.applied());
+    }
+    if (e != Dev::kOk) {
       arena_ = nullptr;
       return e;
     }
@@ -121,7 +130,7 @@ class BounceRing {
     if (!pool_) {
       const char *t = getenv("MIPGPU_COPY_THREADS");  // tuning knob: host copy threads
       threads_ = t && atoi(t) >= 1 && atoi(t) <= 64 ? atoi(t) : 8;
-      pool_.reset(new CopyPool(threads_));
+      pool_.reset(new CopyPool(threads_, place_));
     }
     if (!worker_.joinable()) worker_ = std::thread([this] { complete_loop(); });
     return Dev::kOk;
@@ -223,6 +232,7 @@ class BounceRing {
   // part, finished_, stays valid while the caller retires finished parts at the front.
   void complete_loop() {
     dev_.bind_thread(device_);
+    (void)bind_current_thread(place_);
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
       cv_work_.wait(lk, [&] { return stop_ || finished_ - popped_ < fifo_.size(); });
@@ -373,6 +383,7 @@ class BounceRing {
   }
   Dev dev_;
   int device_ = 0;
+  NumaPlace place_;
   int threads_ = 0;
   double t_up_ = 0, t_down_ = 0, t_wait_ = 0, t_full_ = 0, b_up_ = 0, b_down_ = 0;
   char *arena_ = nullptr;

@@ -14,7 +14,9 @@ struct HipStageDev {
   using Event = hipEvent_t;
   static constexpr Err kOk = hipSuccess;
   static constexpr Err kNotReady = hipErrorNotInitialized;
-  Err host_alloc(char **p, size_t n) { return hipHostMalloc((void **)p, n, hipHostMallocDefault); }
+  Err host_alloc(char **p, size_t n, bool numa_user) {
+    return hipHostMalloc((void **)p, n, numa_user ? hipHostMallocNumaUser : hipHostMallocDefault);
+  }
   void host_free(char *p) { (void)hipHostFree(p); }
   Err event_create(Event *e) { return hipEventCreateWithFlags(e, hipEventDisableTiming); }
   void event_destroy(Event e) { (void)hipEventDestroy(e); }

@@ -116,6 +116,10 @@ struct SearchArgs {
   // (check_refs) 1 to status[kStatusRefs].  status is engine-owned page-locked host memory
   // (read by the host after the search; only ever written when the contract is broken).
   uint32_t *status;
+  // Merged host-pipeline chunks (several host-API calls in one launch, mipgpu.cpp
+  // open_chunk): frame f of the launch marks frame_status[f] (its own call's status set)
+  // instead of status; null otherwise.  Read only when the contract is broken.
+  uint32_t *const *frame_status;
   int check_refs;
   // 16-wave launches with the longest-first order and original references (pair mode,
   // mip_search.hip pair_loop): the first `nonempty` queue positions hold the items with

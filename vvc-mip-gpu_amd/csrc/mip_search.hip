@@ -1345,13 +1345,14 @@ struct WindowStager {
 // loaded chunks) marks the search's status word (SearchArgs::status); the costs of such a
 // frame are not the reference's (the packed 16-bit / f16 arithmetic is sized for 10 bits), so
 // the host reports the search as failed.  Rare path: one plain store per offending thread.
-__device__ __forceinline__ void flag_above_10_bits(uint32_t bits, uint32_t *status, int word) {
-  if (bits & kAbove10Bits) status[word] = 1u;
+// Merged chunks (SearchArgs::frame_status): the frame's own call's status set.
+__device__ __forceinline__ void flag_above_10_bits(uint32_t bits, const SearchArgs &a, int frame, int word) {
+  if (bits & kAbove10Bits) (a.frame_status ? a.frame_status[frame] : a.status)[word] = 1u;
 }
 
 template <int NT>
 __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame, int width, int height,
-                                           int x0, int y0, uint32_t *status) {
+                                           int x0, int y0, const SearchArgs &a, int fidx) {
   const WindowStager<NT> st(frame, width, height, x0, y0, (int)threadIdx.x);
   constexpr int N = WindowStager<NT>::N;
   uint2 v[N];
@@ -1365,7 +1366,7 @@ __device__ __forceinline__ void stage_tile(uint16_t *dst, const uint16_t *frame,
       bits |= v[k].x | v[k].y;
       st.store(dst, k, v[k]);
     }
-  flag_above_10_bits(bits, status, kStatusOrig);
+  flag_above_10_bits(bits, a, fidx, kStatusOrig);
 }
 
 // Item = (frame, CTU, quadrant, slice) -> quadrant origin in the frame and frame index.
@@ -1399,7 +1400,7 @@ struct ItemPos {
 // so a chunk's frame column is its x modulo the width.
 template <int NT>
 __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *frame, int width, int height,
-                                              int x0, int y0, bool check, uint32_t *status) {
+                                              int x0, int y0, bool check, const SearchArgs &a, int fidx) {
   // all loads first, then all LDS stores (as stage_tile)
   constexpr int kChunks = kPitch / 4, NR = 16 * kChunks, NC = 16 * 65;
   constexpr int NRL = (NR + NT - 1) / NT, NCL = (NC + NT - 1) / NT;
@@ -1440,7 +1441,7 @@ __device__ __forceinline__ void stage_lattice(uint16_t *dst, const uint16_t *fra
       if (!(exempt_last && fx >= 0 && frame_col(fx) == width - 1)) bits |= cv[k];
     }
   }
-  if (check) flag_above_10_bits(bits, status, kStatusRefs);
+  if (check) flag_above_10_bits(bits, a, fidx, kStatusRefs);
 }
 
 // Next-item prefetch (PF, non-ALT): two quadrant windows in LDS.  The first wave of an item
@@ -1566,7 +1567,7 @@ __device__ __forceinline__ void stamp_item_start(uint64_t *clk) {
 template <int NT>
 __device__ __forceinline__ void stage_tiles2(uint16_t *dst0, const uint16_t *frame0, int x0, int y0, uint16_t *dst1,
                                              const uint16_t *frame1, int x1, int y1, bool b, int width, int height,
-                                             uint32_t *status) {
+                                             const SearchArgs &a, int f0, int f1) {
   const WindowStager<NT> s0(frame0, width, height, x0, y0, (int)threadIdx.x);
   const WindowStager<NT> s1(frame1, width, height, x1, y1, (int)threadIdx.x);
   constexpr int N = WindowStager<NT>::N;
@@ -1576,19 +1577,20 @@ __device__ __forceinline__ void stage_tiles2(uint16_t *dst0, const uint16_t *fra
     if (s0.valid(k)) v0[k] = s0.load(k);
     if (b && s1.valid(k)) v1[k] = s1.load(k);
   }
-  uint32_t bits = 0;
+  uint32_t bits0 = 0, bits1 = 0;
 #pragma unroll
   for (int k = 0; k < N; k++) {
     if (s0.valid(k)) {
-      bits |= v0[k].x | v0[k].y;
+      bits0 |= v0[k].x | v0[k].y;
       s0.store(dst0, k, v0[k]);
     }
     if (b && s1.valid(k)) {
-      bits |= v1[k].x | v1[k].y;
+      bits1 |= v1[k].x | v1[k].y;
       s1.store(dst1, k, v1[k]);
     }
   }
-  flag_above_10_bits(bits, status, kStatusOrig);
+  flag_above_10_bits(bits0, a, f0, kStatusOrig);
+  flag_above_10_bits(bits1, a, f1, kStatusOrig);
 }
 
 // Pair mode (16-wave workgroups, one per CU; one-frame launches with original references and
@@ -1626,7 +1628,7 @@ __device__ __forceinline__ void pair_loop(const SearchArgs &a, uint16_t *org_buf
     uint16_t *org0 = org_buf, *org1 = org_buf + kTileElems;
     stage_tiles2<64 * kWideWaves>(org0, a.orig + (size_t)p0.frame * a.width * a.height, p0.fx0, p0.fy0, org1,
                                   a.orig + (size_t)p1.frame * a.width * a.height, p1.fx0, p1.fy0, two, a.width,
-                                  a.height, a.status);
+                                  a.height, a, p0.frame, p1.frame);
     __syncthreads();
     uint64_t *clk0 = a.wave_clock ? a.wave_clock + (size_t)i0 * kClockSlots : nullptr;
     uint64_t *clk1 = a.wave_clock && two ? a.wave_clock + (size_t)i1 * kClockSlots : nullptr;
@@ -1730,8 +1732,8 @@ __global__ __launch_bounds__(64 * NW, NW == kWideWaves ? 4 : MIP_WAVES_PER_EU) v
     fill_unavailable<DEC>(a, frame, ctu, vq, slice);
     if (ntasks > 0) {  // workgroup-uniform
       if (!PF || !staged) {
-        stage_tile<64 * NW>(org, a.orig + fofs, a.width, a.height, fx0, fy0, a.status);
-        if (ALT) stage_lattice<64 * NW>(ref, a.refs + fofs, a.width, a.height, fx0, fy0, a.check_refs != 0, a.status);
+        stage_tile<64 * NW>(org, a.orig + fofs, a.width, a.height, fx0, fy0, a, frame);
+        if (ALT) stage_lattice<64 * NW>(ref, a.refs + fofs, a.width, a.height, fx0, fy0, a.check_refs != 0, a, frame);
         __syncthreads();
       }
 
@@ -1804,7 +1806,7 @@ __global__ __launch_bounds__(64 * NW, NW == kWideWaves ? 4 : MIP_WAVES_PER_EU) v
                 st.store(dst, k0 + k, v[k]);
               }
           }
-          flag_above_10_bits(bits, a.status, kStatusOrig);
+          flag_above_10_bits(bits, a, np.frame, kStatusOrig);
         }
         if (lane == 0) {
           nxt[0] = 0;

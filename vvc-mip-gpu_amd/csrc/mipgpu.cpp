@@ -8,18 +8,22 @@
 #include <functional>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mip_kernels.h"
 #include "mip_tables.h"
 #include "chunk_plan.h"
 #include "host_stage_hip.h"
+#include "numa_place.h"
 #include "queue_ring.h"
 
 namespace {
@@ -486,6 +490,9 @@ bool filter_valid(int f, int k) {
 
 struct mip_engine {
   int device = 0, width = 0, height = 0, nctus = 0, ctu_cols = 0;
+  // NUMA placement of the engine's host side (numa_place.h): its GPU's node, whose memory
+  // holds the engine's page-locked buffers and whose CPUs run its host threads.
+  mipgpu::NumaPlace place;
   mip_opts opts{};
   // Host API pipeline (mip_search_frames): `stream` and `stream4` compute (chunks alternate
   // between them, so that one chunk's search takes the CUs its predecessor's drains), `stream2`
@@ -606,7 +613,45 @@ struct mip_engine {
   // 1 = frame samples, 2 = reference samples).
   uint32_t *h_status = nullptr, *d_status = nullptr;
   uint64_t status_harvested = 0;
-  std::map<uint64_t, uint32_t> call_errors;
+  std::map<uint64_t, uint32_t> call_errors;  // (4: the call's merged launch failed)
+
+  // Merged chunks (round 6).  A small host-API call (page-locked buffers, fewer frames than a
+  // slot) that arrives while the pipeline is busy is not launched on its own: it opens -- or
+  // joins -- the *open chunk*, whose frames are uploaded into one slot's region at the
+  // calls' offsets as they arrive, and the chunk is searched by ONE launch of all its frames
+  // (open_chunk / flush_open).  One-frame launches run at 0.177 ms against 0.13 ms per frame
+  // in 4-frame launches (profiles/r05_small_batch_final.jsonl), so per-frame callers (the
+  // reference's loop, main.cpp:678-1241) queueing calls get the multi-frame rate.  The chunk
+  // is launched when it is full (slot frames or kMergeCalls calls), when a call that cannot
+  // join it arrives, at any mip_wait or synchronous call, before any device-API work of the
+  // engine, and -- by the engine's flusher thread -- as soon as the search launched before
+  // it has completed, so a call never waits for later calls.  MIPGPU_MERGE=0 (A/B knob): off.
+  static constexpr int kMergeCalls = 32;
+  struct Member {
+    uint64_t call;
+    int f0, n;  // frames [f0, f0 + n) of the chunk
+    int32_t *costs, *sad, *satd, *best_cost;
+    uint8_t *best_mode;
+  };
+  struct OpenChunk {
+    bool active = false;
+    uint64_t k = 0;       // chunk sequence number (slot k % hp_slots)
+    uint64_t serial = 0;  // counts opened chunks (the flusher's "still the same chunk?")
+    int nb = 0;           // frames so far
+    unsigned sig = 0;     // outputs and reference source of its calls (merge_sig)
+    std::vector<Member> members;
+  } open;
+  int last_slot = -1;  // slot of the last launched host-pipeline chunk (its slot_comp event)
+  uint64_t stat_launches = 0, stat_merged_calls = 0, stat_merged_launches = 0;  // mip_host_stats
+  // per-frame status pointers of merged launches ([kCallRing][hp_cap], page-locked, mapped;
+  // row (first call - 1) % kCallRing), SearchArgs::frame_status
+  uint32_t **h_frame_status = nullptr, **d_frame_status = nullptr;
+  // Every public entry point that uses the engine holds `mu` (the flusher thread shares the
+  // engine's streams and state).
+  std::recursive_mutex mu;
+  std::condition_variable_any flush_cv;
+  std::thread flusher;
+  bool flusher_stop = false;
 };
 
 namespace {
@@ -772,6 +817,19 @@ static int wait_refs_readers(mip_engine *e) {
   return 0;
 }
 
+// Launch the engine's open (merged) chunk, if any (defined with the host pipeline below).
+static int flush_open(mip_engine *e);
+
+// NUMA placement of a device (numa_place.h; none when the bus id or its node is unknown).
+static mipgpu::NumaPlace device_place(int device) {
+  char bus[64] = {};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return mipgpu::NumaPlace();
+  }
+  return mipgpu::numa_place_of_pci(bus);
+}
+
 extern "C" {
 
 void mip_opts_default(mip_opts *o) {
@@ -840,6 +898,14 @@ int mip_cu_position(int shape, int cu, int *x, int *y) {
 
 int mip_engine_destroy(mip_engine *e) {
   if (!e) return 0;
+  {  // the open chunk is launched (its calls were accepted), then the flusher stops
+    std::lock_guard<std::recursive_mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    (void)flush_open(e);
+    e->flusher_stop = true;
+  }
+  e->flush_cv.notify_all();
+  if (e->flusher.joinable()) e->flusher.join();
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
@@ -856,6 +922,7 @@ int mip_engine_destroy(mip_engine *e) {
   }
   if (e->d_queue) (void)hipFree(e->d_queue);
   if (e->h_status) (void)hipHostFree(e->h_status);
+  if (e->h_frame_status) (void)hipHostFree(e->h_frame_status);
   for (hipEvent_t ev : e->queue_done)
     if (ev) (void)hipEventDestroy(ev);
   if (e->refs_done) (void)hipEventDestroy(e->refs_done);
@@ -912,7 +979,9 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
 
   mip_engine *e = new mip_engine();
   e->device = device;
+  e->place = device_place(device);
   e->stage.set_device(device);  // (the bounce ring's completion thread)
+  e->stage.set_place(e->place);
   e->width = width;
   e->height = height;
   e->nctus = mip_num_ctus(width, height);
@@ -982,7 +1051,7 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
     return cleanup(fail("hipMemset failed"));
   // Every engine stream takes its hardware queue now, and the copy streams their copy
   // engines (1 MiB each way through a page-locked buffer): HIP sets these up at their first
-  // use (tools/_r05ao.sh: the CLI's first download started 8-9 ms after the search it
+  // use (tools/experiments/r05/_r05ao.sh: the CLI's first download started 8-9 ms after the search it
   // waited for).  (The counters are zero: rewriting one is harmless.)
   {
     void *h = nullptr;
@@ -1001,11 +1070,23 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   for (hipEvent_t &ev : e->queue_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   const size_t status_bytes = (size_t)(mip_engine::kCallRing + 1) * mipgpu::kStatusWords * sizeof(uint32_t);
-  if (hipHostMalloc((void **)&e->h_status, status_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+  const mipgpu::ScopedNodePolicy pol(e->place);  // (the engine's page-locked words on its node)
+  const unsigned numa_flag = pol.applied() ? hipHostMallocNumaUser : 0u;
+  if (hipHostMalloc((void **)&e->h_status, status_bytes, hipHostMallocMapped | hipHostMallocCoherent | numa_flag) !=
+      hipSuccess)
     return cleanup(fail("hipHostMalloc (status words) failed"));
   memset(e->h_status, 0, status_bytes);
   if (hipHostGetDevicePointer((void **)&e->d_status, e->h_status, 0) != hipSuccess || !e->d_status)
     return cleanup(fail("hipHostGetDevicePointer (status words) failed"));
+  {  // merged chunks' per-frame status pointers (mip_engine::h_frame_status)
+    const size_t bytes = (size_t)mip_engine::kCallRing * e->hp_cap * sizeof(uint32_t *);
+    if (hipHostMalloc((void **)&e->h_frame_status, bytes, hipHostMallocMapped | hipHostMallocCoherent | numa_flag) !=
+        hipSuccess)
+      return cleanup(fail("hipHostMalloc (frame status) failed"));
+    memset(e->h_frame_status, 0, bytes);
+    if (hipHostGetDevicePointer((void **)&e->d_frame_status, e->h_frame_status, 0) != hipSuccess || !e->d_frame_status)
+      return cleanup(fail("hipHostGetDevicePointer (frame status) failed"));
+  }
   if (hipEventCreateWithFlags(&e->refs_done, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail("hipEventCreate failed"));
   for (int alt = 0; alt < 2; alt++) {
@@ -1137,7 +1218,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
                               int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best,
                               int32_t *d_best_cost, hipStream_t s, bool caller_refs, uint32_t *d_status,
                               int ctu0 = 0, int nrange = -1, uint32_t *split_acc = nullptr,
-                              mipgpu::SplitArgs *defer_split = nullptr, hipEvent_t *done = nullptr) {
+                              mipgpu::SplitArgs *defer_split = nullptr, hipEvent_t *done = nullptr,
+                              uint32_t *const *frame_status = nullptr) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
   // Decisions only (no cost table): the search writes each CU's decision into d_best /
   // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
@@ -1196,6 +1278,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.nrange = nrange;
   a.slices = work.slices;
   a.status = d_status;  // the calling API's status set (mip_engine::h_status)
+  a.frame_status = frame_status;  // merged chunks: each frame's own call's set
   a.check_refs = alt && caller_refs;
   a.order = lpt_order_enabled() ? work.d_order : nullptr;  // launch_search drops it for large / range launches
   // pair mode of 16-wave launches (original references; launch_search checks the rest)
@@ -1281,14 +1364,17 @@ int mip_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d
                       int32_t *d_costs, int32_t *d_sad, int32_t *d_satd, uint8_t *d_best_mode,
                       int32_t *d_best_cost, void *stream) {
   if (!e) return fail("engine is NULL");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   if (check_device_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
+  if (flush_open(e) != 0) return -1;  // (device-API work orders itself after the host calls)
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, d_best_mode, d_best_cost,
                             (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames, device_status(e));
 }
 
 int mip_check_input(mip_engine *e, void *stream) {
   if (!e) return fail("engine is NULL");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   return check_device_status(e);
@@ -1298,11 +1384,13 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
                             int ctu_begin, int ctu_end, int32_t *d_costs, int32_t *d_sad, int32_t *d_satd,
                             void *stream) {
   if (!e) return fail("engine is NULL");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   if (!d_costs) return fail("d_costs is NULL");
   // an empty range (more CTU-row bands than CTU rows, mipgpu.split) is a successful no-op
   if (ctu_begin == ctu_end && ctu_begin >= 0 && ctu_end <= e->nctus) return 0;
   if (check_device_status(e) != 0) return -1;
   HIP_TRY(hipSetDevice(e->device));
+  if (flush_open(e) != 0) return -1;
   return search_device_impl(e, d_frames, d_refs, nframes, d_costs, d_sad, d_satd, nullptr, nullptr,
                             (hipStream_t)stream, d_refs != nullptr && d_refs != d_frames, device_status(e), ctu_begin,
                             ctu_end - ctu_begin);
@@ -1328,12 +1416,164 @@ static int drain_trace(mip_engine *e, int sl) {
   return 0;
 }
 
+// ---- Merged chunks (mip_engine::open, round 6) ----
+// Outputs and reference source of a host-API call: calls merge into one launch only when
+// these agree (one kernel variant, one set of output tables for the chunk).
+enum : unsigned { kSigCost = 1, kSigSad = 2, kSigSatd = 4, kSigBestMode = 8, kSigBestCost = 16, kSigRefs = 32, kSigDec = 64 };
+
+// MIPGPU_MERGE (A/B / test knob): 0 = every call launches on its own; "hold" = small calls
+// open a chunk even into an idle pipeline and the flusher thread never launches it (only the
+// other triggers do: deterministic merges for tests).
+static int merge_mode() {
+  const char *e = getenv("MIPGPU_MERGE");
+  if (e && *e == '0') return 0;
+  return e && !strcmp(e, "hold") ? 2 : 1;
+}
+
+// Launch the open chunk: the engine filter over its frames (engine references), ONE search
+// of all its frames -- each frame marking its own call's status set (SearchArgs::frame_status)
+// -- each member call's downloads from its own frames, and each member call's completion
+// event.  After a failure the members' tickets report it (call_errors flag 4).
+static int flush_open(mip_engine *e) {
+  mip_engine::OpenChunk &o = e->open;
+  if (!o.active) return 0;
+  o.active = false;  // (whatever happens below, the chunk is over)
+  if (o.members.empty()) return 0;
+  const uint64_t k = o.k, first = o.members.front().call;
+  const int sl = (int)(k % e->hp_slots), nb = o.nb;
+  const unsigned sig = o.sig;
+  const bool dec = (sig & kSigDec) != 0;
+  const size_t fs = (size_t)e->width * e->height, fo = (size_t)sl * e->hp_cap;
+  const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
+  const hipStream_t up = e->stream2, down = e->stream3;
+  const hipStream_t comp = search_streams() == 2 && (k & 1) ? e->stream4 : e->stream;
+  auto run = [&]() -> int {
+    uint16_t *d_frames = e->d_frames + fo * fs;
+    const uint16_t *d_refs = (sig & kSigRefs) ? e->d_refs + fo * fs : nullptr;
+    if (!(sig & kSigRefs) && e->opts.filter != MIP_FILTER_NONE) {  // on the upload stream, as a chunk's
+      if (mip_filter_device(d_frames, e->d_refs + fo * fs, e->width, e->height, nb, e->opts.filter, e->opts.kernel_idx,
+                            up) != 0)
+        return -1;
+      d_refs = e->d_refs + fo * fs;
+    }
+    HIP_TRY(hipEventRecord(e->slot_up[sl], up));
+    HIP_TRY(hipStreamWaitEvent(comp, e->slot_up[sl], 0));
+    // row (first - 1) % kCallRing: its previous user, the chunk of call first - kCallRing, has
+    // completed (search_frames_call waits for that call before accepting call `first`)
+    const size_t row = (size_t)((first - 1) % mip_engine::kCallRing) * e->hp_cap;
+    for (const mip_engine::Member &m : o.members)
+      for (int i = 0; i < m.n; i++) e->h_frame_status[row + m.f0 + i] = call_status(e, m.call);
+    int32_t *d_costs = dec ? nullptr : e->d_costs + fo * cpf;
+    int32_t *d_sad = (sig & kSigSad) ? e->d_sad + fo * cpf : nullptr;
+    int32_t *d_satd = (sig & kSigSatd) ? e->d_satd + fo * cpf : nullptr;
+    uint8_t *d_best = (sig & kSigBestMode) ? e->d_best + fo * upf : nullptr;
+    int32_t *d_best_cost = (sig & kSigBestCost) || dec ? e->d_best_cost + fo * upf : nullptr;
+    mipgpu::SplitArgs split{};
+    const bool defer = dec && !dec_inline();
+    hipEvent_t comp_done = e->slot_comp[sl];
+    if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
+                           (sig & kSigRefs) != 0, call_status(e, first), 0, -1,
+                           defer ? e->d_split_acc + fo * e->nctus * MIP_CUS_PER_CTU : nullptr, defer ? &split : nullptr,
+                           &comp_done, e->d_frame_status + row) != 0)
+      return -1;
+    if (comp_done) HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
+    e->last_slot = sl;
+    e->stat_launches++;
+    e->stat_merged_launches++;
+    e->stat_merged_calls += o.members.size();
+    HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));
+    if (defer) HIP_TRY(mipgpu::launch_dec_split(split, nb, false, down));
+    for (const mip_engine::Member &m : o.members) {
+      const size_t f = (size_t)m.f0, n = (size_t)m.n;
+      if (m.costs) HIP_TRY(hipMemcpyAsync(m.costs, d_costs + f * cpf, n * cpf * 4, hipMemcpyDeviceToHost, down));
+      if (m.sad) HIP_TRY(hipMemcpyAsync(m.sad, d_sad + f * cpf, n * cpf * 4, hipMemcpyDeviceToHost, down));
+      if (m.satd) HIP_TRY(hipMemcpyAsync(m.satd, d_satd + f * cpf, n * cpf * 4, hipMemcpyDeviceToHost, down));
+      if (m.best_mode) HIP_TRY(hipMemcpyAsync(m.best_mode, d_best + f * upf, n * upf, hipMemcpyDeviceToHost, down));
+      if (m.best_cost)
+        HIP_TRY(hipMemcpyAsync(m.best_cost, d_best_cost + f * upf, n * upf * 4, hipMemcpyDeviceToHost, down));
+    }
+    HIP_TRY(hipEventRecord(e->slot_down[sl], down));
+    return 0;
+  };
+  const int rc = run();
+  if (rc != 0) {  // (as a failed call: wait for what was queued, restore the split accumulator)
+    const std::string err = g_err;
+    for (hipStream_t st : {e->stream2, e->stream, e->stream4, e->stream3}) (void)hipStreamSynchronize(st);
+    (void)hipMemset(e->d_split_acc, 0xff, (size_t)e->hp_frames * e->nctus * MIP_CUS_PER_CTU * 4);
+    g_err = err;
+  }
+  for (const mip_engine::Member &m : o.members) {  // completion of every member (its ticket)
+    if (rc != 0) e->call_errors[m.call] |= 4u;
+    (void)hipEventRecord(e->call_done[(m.call - 1) % mip_engine::kCallRing], down);
+  }
+  o.members.clear();
+  o.nb = 0;
+  return rc;
+}
+
+// The engine's flusher thread: launches an open chunk as soon as the search launched before
+// it has completed (a merged call never waits for later calls; calls that arrive meanwhile
+// join the chunk).  Started with the first open chunk; stopped by mip_engine_destroy.
+static void flusher_loop(mip_engine *e) {
+  (void)hipSetDevice(e->device);
+  (void)mipgpu::bind_current_thread(e->place);
+  std::unique_lock<std::recursive_mutex> lk(e->mu);
+  uint64_t seen = 0;
+  for (;;) {
+    e->flush_cv.wait(lk, [&] { return e->flusher_stop || (e->open.active && e->open.serial != seen); });
+    if (e->flusher_stop) return;
+    const uint64_t serial = seen = e->open.serial;
+    if (e->last_slot >= 0) {
+      // (the event may be recorded again meanwhile, for a later chunk: then the wait only ends
+      // later -- by then the open chunk has been launched by its owner's calls)
+      const hipEvent_t ev = e->slot_comp[e->last_slot];
+      lk.unlock();
+      (void)hipEventSynchronize(ev);
+      lk.lock();
+    }
+    if (e->open.active && e->open.serial == serial) (void)flush_open(e);
+  }
+}
+
+// Add a call to the open chunk (opening one if there is none): its frames (and caller
+// references) are uploaded into the chunk's slot region at the chunk's next frame.
+static int merge_call(mip_engine *e, const uint16_t *frames, const uint16_t *refs, int nframes, int32_t *costs,
+                      uint8_t *best_mode, int32_t *best_cost, int32_t *sad, int32_t *satd, unsigned sig, uint64_t call) {
+  mip_engine::OpenChunk &o = e->open;
+  const size_t fs = (size_t)e->width * e->height;
+  const hipStream_t up = e->stream2;
+  if (!o.active) {
+    if ((refs || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
+      HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
+    if (wait_refs_readers(e) != 0) return -1;
+    e->refs_pending = false;
+    o.k = e->host_chunks++;
+    const int sl = (int)(o.k % e->hp_slots);
+    o.active = true;
+    o.serial++;
+    o.nb = 0;
+    o.sig = sig;
+    o.members.clear();
+    // the slot's previous chunk is over once its downloads are (as search_frames_chunks)
+    if (o.k >= (uint64_t)e->hp_slots) HIP_TRY(hipStreamWaitEvent(up, e->slot_down[sl], 0));
+    if (!e->flusher.joinable() && merge_mode() != 2) e->flusher = std::thread(flusher_loop, e);
+    e->flush_cv.notify_all();
+  }
+  const size_t f = (size_t)(o.k % e->hp_slots) * e->hp_cap + o.nb;
+  HIP_TRY(hipMemcpyAsync(e->d_frames + f * fs, frames, nframes * fs * 2, hipMemcpyHostToDevice, up));
+  if (refs) HIP_TRY(hipMemcpyAsync(e->d_refs + f * fs, refs, nframes * fs * 2, hipMemcpyHostToDevice, up));
+  o.members.push_back(mip_engine::Member{call, o.nb, nframes, costs, sad, satd, best_cost, best_mode});
+  o.nb += nframes;
+  return 0;
+}
+
 // One host-API call (mip_search_frames_async; mip_search_frames with sync = true: it waits for
 // the call before returning, so no later call can queue behind its last chunks).
 static int search_frames_call(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                               int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
                               int32_t *satd_out, uint64_t *ticket, bool sync) {
   if (!e || !frames || nframes < 1 || !ticket) return fail("bad search arguments");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   *ticket = 0;
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
   HIP_TRY(hipSetDevice(e->device));
@@ -1341,8 +1581,46 @@ static int search_frames_call(mip_engine *e, const uint16_t *frames, const uint1
   // call `next` marks status set (next - 1) % kCallRing: the call that used it before (more
   // than kCallRing calls in flight) must have completed and been harvested first
   if (next > (uint64_t)mip_engine::kCallRing && e->status_harvested < next - mip_engine::kCallRing) {
+    if (e->open.active && e->open.members.front().call <= next - mip_engine::kCallRing && flush_open(e) != 0) return -1;
     HIP_TRY(hipEventSynchronize(e->call_done[(next - 1) % mip_engine::kCallRing]));
     harvest_status(e, next - mip_engine::kCallRing);
+  }
+  // Merged chunks (mip_engine::open): a call with page-locked buffers and fewer frames than a
+  // slot joins the open chunk (same outputs, room left), or opens one while the pipeline is
+  // busy; anything else launches the open chunk first and takes the chunked path.
+  {
+    using mipgpu::host_pinned;
+    const bool pinned = host_pinned(frames) && (!refs_or_null || host_pinned(refs_or_null)) &&
+                        (!costs_out || host_pinned(costs_out)) && (!sad_out || host_pinned(sad_out)) &&
+                        (!satd_out || host_pinned(satd_out)) && (!best_mode_out || host_pinned(best_mode_out)) &&
+                        (!best_cost_out || host_pinned(best_cost_out));
+    const bool dec = !costs_out && !sad_out && !satd_out && e->opts.best_k == 1 && (best_mode_out || best_cost_out);
+    const unsigned sig = (costs_out ? kSigCost : 0) | (sad_out ? kSigSad : 0) | (satd_out ? kSigSatd : 0) |
+                         (best_mode_out ? kSigBestMode : 0) | (best_cost_out ? kSigBestCost : 0) |
+                         (refs_or_null ? kSigRefs : 0) | (dec ? kSigDec : 0);
+    const int mode = merge_mode();
+    const bool small = pinned && mode && !e->trace && nframes < e->hp_cap;
+    mip_engine::OpenChunk &o = e->open;
+    bool join = false;
+    if (o.active) {
+      join = small && o.sig == sig && o.nb + nframes <= e->hp_cap && (int)o.members.size() < mip_engine::kMergeCalls;
+      if (!join && flush_open(e) != 0) return -1;
+    }
+    if (!o.active && small && !sync &&
+               (mode == 2 || (e->host_calls > 0 && hipEventQuery(e->call_done[(e->host_calls - 1) %
+                                                                              mip_engine::kCallRing]) == hipErrorNotReady))) {
+      join = true;  // the pipeline is busy: open a chunk
+    }
+    if (join) {
+      if (merge_call(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out, sad_out, satd_out, sig,
+                     next) != 0)
+        return -1;
+      *ticket = ++e->host_calls;
+      e->host_pending = true;
+      if ((o.nb >= e->hp_cap || (int)o.members.size() >= mip_engine::kMergeCalls || sync) && flush_open(e) != 0)
+        return -1;
+      return 0;
+    }
   }
   const int rc = search_frames_chunks(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out,
                                       sad_out, satd_out, next, sync);
@@ -1561,6 +1839,8 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
                            defer ? &split : nullptr, &comp_done) != 0)
       return -1;
     if (comp_done) HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
+    e->last_slot = sl;
+    e->stat_launches++;
     HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));  // (also without outputs: slot_down ends the chunk)
     if (defer) HIP_TRY(mipgpu::launch_dec_split(split, nb, false, down));
     if (costs_out) HIP_TRY(to_host(costs_out + f0 * cpf, d_costs, nb * cpf * 4, pin_cost));
@@ -1576,8 +1856,12 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
 
 int mip_wait(mip_engine *e, uint64_t ticket) {
   if (!e) return fail("engine is NULL");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   if (ticket == 0 || ticket > e->host_calls) return fail("unknown ticket %llu", (unsigned long long)ticket);
   HIP_TRY(hipSetDevice(e->device));
+  // the caller is about to block: an open chunk can gain no more calls from it (launched now,
+  // behind the searches in flight; a failure is reported by its members' tickets)
+  (void)flush_open(e);
   // a ticket older than the ring shares its event with a later call: waiting for that one
   // is later than needed, never too early
   HIP_TRY(hipEventSynchronize(e->call_done[(ticket - 1) % mip_engine::kCallRing]));
@@ -1590,6 +1874,8 @@ int mip_wait(mip_engine *e, uint64_t ticket) {
   if (it == e->call_errors.end()) return 0;
   const uint32_t f = it->second;
   e->call_errors.erase(it);
+  if (f & 4u)
+    return fail("host-API call %llu of this engine: its merged launch failed", (unsigned long long)ticket);
   char what[64];
   snprintf(what, sizeof what, "host-API call %llu of this engine", (unsigned long long)ticket);
   return contract_error(f, what);
@@ -1598,6 +1884,8 @@ int mip_wait(mip_engine *e, uint64_t ticket) {
 int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null, int nframes,
                       int32_t *costs_out, uint8_t *best_mode_out, int32_t *best_cost_out, int32_t *sad_out,
                       int32_t *satd_out) {
+  if (!e) return fail("engine is NULL");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   uint64_t ticket = 0;
   if (search_frames_call(e, frames, refs_or_null, nframes, costs_out, best_mode_out, best_cost_out, sad_out,
                          satd_out, &ticket, true) != 0)
@@ -1607,7 +1895,9 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
 
 int mip_trace_times(mip_engine *e, int enable) {
   if (!e) return fail("engine is NULL");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->device));
+  if (flush_open(e) != 0) return -1;  // (merged chunks are not traced)
   if (enable && !e->tr_ev[0][0]) {
     // all events or none: a partial set would turn tracing on with null events
     hipEvent_t ev[mip_engine::kHostSlots][4] = {};
@@ -1627,6 +1917,7 @@ int mip_trace_times(mip_engine *e, int enable) {
 
 int mip_pop_times(mip_engine *e, double *upload_ms, double *filter_ms, int max, int *n) {
   if (!e || !n || max < 0) return fail("bad arguments");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->device));
   // pending chunks in sequence order (frame order)
   std::vector<int> order;
@@ -1645,12 +1936,38 @@ int mip_pop_times(mip_engine *e, double *upload_ms, double *filter_ms, int max, 
   return 0;
 }
 
+int mip_host_stats(mip_engine *e, uint64_t *out, int n) {
+  if (!e || !out || n < 0 || n > 4) return fail("bad arguments");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  const uint64_t v[4] = {e->host_calls, e->stat_launches, e->stat_merged_calls, e->stat_merged_launches};
+  for (int i = 0; i < n; i++) out[i] = v[i];
+  return 0;
+}
+
 int mip_host_alloc(size_t bytes, void **out) {
   if (!out) return fail("out is NULL");
   *out = nullptr;
   HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
   return 0;
 }
+
+int mip_host_alloc_near(int device, size_t bytes, void **out) {
+  if (!out) return fail("out is NULL");
+  *out = nullptr;
+  const mipgpu::NumaPlace p = device_place(device);
+  const mipgpu::ScopedNodePolicy pol(p);
+  HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, pol.applied() ? hipHostMallocNumaUser : hipHostMallocDefault));
+  return 0;
+}
+
+int mip_numa_node_of_pci(const char *pci_bus_id) {
+  if (!pci_bus_id) return fail("pci_bus_id is NULL");
+  return mipgpu::numa_place_of_pci(pci_bus_id).node;
+}
+
+int mip_numa_node(int device) { return device_place(device).node; }
+
+int mip_bind_thread(int device) { return mipgpu::bind_current_thread(device_place(device)) ? 1 : 0; }
 
 int mip_host_free(void *p) {
   if (p) HIP_TRY(hipHostFree(p));
@@ -1660,7 +1977,9 @@ int mip_host_free(void *p) {
 int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int filter, int kernel_idx,
                       uint16_t *out) {
   if (!e || !frames || !out || nframes < 1) return fail("bad filter arguments");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->device));
+  if (flush_open(e) != 0) return -1;
   const size_t fs = (size_t)e->width * e->height;
   if (!e->d_refs) HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
   if (wait_refs_readers(e) != 0) return -1;
@@ -1685,7 +2004,9 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
 double mip_time_search_device(mip_engine *e, const uint16_t *d_frames, const uint16_t *d_refs, int nframes,
                               int32_t *d_costs, int reps) {
   if (!e || reps < 1) return fail("bad timing arguments");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
   if (hipSetDevice(e->device) != hipSuccess) return fail("hipSetDevice");
+  if (flush_open(e) != 0) return -1;
   hipEvent_t t0, t1;
   if (hipEventCreate(&t0) != hipSuccess || hipEventCreate(&t1) != hipSuccess) return fail("hipEventCreate");
   (void)hipEventRecord(t0, e->stream);

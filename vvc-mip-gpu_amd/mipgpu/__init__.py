@@ -128,8 +128,13 @@ def library():
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
         "mip_topk_device": (ip, [vp, ip, ip, ip, ip, vp, vp, vp]),
         "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
+        "mip_host_stats": (ip, [vp, ctypes.POINTER(ctypes.c_uint64), ip]),
         "mip_host_alloc": (ip, [ctypes.c_size_t, ctypes.POINTER(vp)]),
         "mip_host_free": (ip, [vp]),
+        "mip_host_alloc_near": (ip, [ip, ctypes.c_size_t, ctypes.POINTER(vp)]),
+        "mip_bind_thread": (ip, [ip]),
+        "mip_numa_node": (ip, [ip]),
+        "mip_numa_node_of_pci": (ip, [ctypes.c_char_p]),
         "mip_last_error": (ctypes.c_char_p, []),
         "mip_abi_version": (ip, []),
         "mip_build_id": (ctypes.c_char_p, []),
@@ -165,13 +170,17 @@ def _ptr(a):
     return a.data_ptr()  # torch tensor
 
 
-def pinned_empty(shape, dtype) -> np.ndarray:
-    """Uninitialised numpy array in page-locked host memory (mip_host_alloc); transfers
-    to / from it run at DMA rate.  The memory is released with the last view of it."""
+def pinned_empty(shape, dtype, device=None) -> np.ndarray:
+    """Uninitialised numpy array in page-locked host memory (mip_host_alloc; with `device`,
+    mip_host_alloc_near: on that GPU's NUMA node); transfers to / from it run at DMA rate.
+    The memory is released with the last view of it."""
     dt = np.dtype(dtype)
     count = int(np.prod(shape))
     p = ctypes.c_void_p()
-    _check(library().mip_host_alloc(max(1, count * dt.itemsize), ctypes.byref(p)))
+    if device is None:
+        _check(library().mip_host_alloc(max(1, count * dt.itemsize), ctypes.byref(p)))
+    else:
+        _check(library().mip_host_alloc_near(int(device), max(1, count * dt.itemsize), ctypes.byref(p)))
     buf = (ctypes.c_byte * max(1, count * dt.itemsize)).from_address(p.value)
     weakref.finalize(buf, library().mip_host_free, ctypes.c_void_p(p.value))
     return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
@@ -327,6 +336,14 @@ class MipEngine:
             _check(library().mip_wait(self._h, ctypes.c_uint64(ticket.value)))
         return ticket.out
 
+    def host_stats(self) -> dict:
+        """Host-pipeline counters (mip_host_stats): calls, search launches, calls that went
+        through merged launches, merged launches."""
+        out = (ctypes.c_uint64 * 4)()
+        with self._lock:
+            _check(library().mip_host_stats(self._h, out, 4))
+        return dict(zip(("calls", "launches", "merged_calls", "merged_launches"), (int(v) for v in out)))
+
     def filter_frames(self, frames, filter, kernel_idx=0):
         f = self._frames(frames)
         out = np.empty_like(f)
@@ -382,6 +399,16 @@ class MipEngine:
         return ms
 
 
+def numa_node(device) -> int:
+    """NUMA node of a GPU (mip_numa_node; -1: unknown or a one-node host)."""
+    return int(library().mip_numa_node(int(device)))
+
+
+def bind_thread(device) -> bool:
+    """Run the calling thread on the CPUs of the GPU's NUMA node (mip_bind_thread)."""
+    return library().mip_bind_thread(int(device)) == 1
+
+
 def unavailable_cus(width, height, filter=None) -> np.ndarray:
     """Bool per CU (reference order): the CUs an engine with this filter reports as
     MIP_COST_UNAVAILABLE (mip_unavailable_cus; host only)."""
@@ -417,5 +444,5 @@ def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
 
 
 __all__ = ["MipEngine", "MipError", "build_id", "source_id", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "topk_device", "library",
-           "pinned_empty", "unavailable_cus",
+           "pinned_empty", "unavailable_cus", "numa_node", "bind_thread",
            "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]
