@@ -145,9 +145,10 @@ int mip_search_frames(mip_engine *e, const uint16_t *frames, const uint16_t *ref
  * slot (opts.max_batch below 16, else max_batch / 4) that arrives while the pipeline is busy
  * joins the engine's open chunk -- calls with the same outputs and reference source share ONE
  * search launch (one-frame calls then run at the multi-frame launch rate).  The chunk is
- * launched when full, when an incompatible call arrives, at any mip_wait / synchronous call /
- * device-API call of the engine, or by the engine's own thread as soon as the search before it
- * has completed.  Every call keeps its own ticket, outputs and input-contract status. */
+ * launched when full, when an incompatible call arrives, when a later call finds the GPU idle,
+ * at any mip_wait / mip_flush / synchronous call / device-API call of the engine.  Every call
+ * keeps its own ticket, outputs and input-contract status.  A caller that queues a call and
+ * then neither waits nor calls again should call mip_flush (launches the open chunk now). */
 int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_t *refs_or_null,
                             int nframes, int32_t *costs_out, uint8_t *best_mode_out,
                             int32_t *best_cost_out, int32_t *sad_out, int32_t *satd_out,
@@ -160,6 +161,9 @@ int mip_search_frames_async(mip_engine *e, const uint16_t *frames, const uint16_
  * if THIS call's search staged a sample above 1023 (input contract; every call has its own
  * status, so an earlier or later call's violation is reported by that call's own wait). */
 int mip_wait(mip_engine *e, uint64_t ticket);
+
+/* Launch the engine's open (merged) chunk now, if any (see mip_search_frames_async); no wait. */
+int mip_flush(mip_engine *e);
 
 /* Device-resident variant (inputs already in HBM; all pointers are device pointers,
  * `stream` is a hipStream_t; NULL means the default (null) stream, as in HIP).

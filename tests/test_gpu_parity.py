@@ -873,9 +873,9 @@ def test_merged_launches_keep_each_call_its_own(gpu_available, monkeypatch, filt
 def test_merged_launches_1080p_default_policy(gpu_available):
     """Default merge policy at the bench size: 24 one-frame 1080p calls queued back to back
     (page-locked, decisions only and full tables in runs) merge while the pipeline is busy;
-    every output equals a synchronous search of the same frame.  Then the flusher thread: a
-    one-frame call queued behind a 4-frame call is launched without any wait (the counters
-    show its merged launch after the 4-frame search has completed)."""
+    every output equals a synchronous search of the same frame.  Then a one-frame call queued
+    behind a 4-frame call stays open after that search has completed, until mip_flush -- or
+    the next call, which finds the GPU idle -- launches it."""
     import time
     from mipgpu import pinned_empty
     W, H = 1920, 1080
@@ -885,29 +885,42 @@ def test_merged_launches_1080p_default_policy(gpu_available):
     with MipEngine(W, H, max_batch=8) as eng:
         pf = pinned_empty(pool.shape, np.uint16)
         pf[:] = pool
-        tickets, kinds = [], []
-        for i in range(24):
-            full = (i // 6) % 2 == 1
-            out = {"best_mode": pinned_empty((1, eng.cus_per_frame), np.uint8),
-                   "best_cost": pinned_empty((1, eng.cus_per_frame), np.int32)}
+
+        def outs(nf, full):
+            o = {"best_mode": pinned_empty((nf, eng.cus_per_frame), np.uint8),
+                 "best_cost": pinned_empty((nf, eng.cus_per_frame), np.int32)}
             if full:
-                out["cost"] = pinned_empty((1, eng.costs_per_frame), np.int32)
-            tickets.append(eng.search_async(pf[i % 4:i % 4 + 1], costs=full, best=True, out=out))
-            kinds.append(full)
-        outs = [eng.wait(t) for t in tickets]
+                o["cost"] = pinned_empty((nf, eng.costs_per_frame), np.int32)
+            return o
+        kinds = [(i // 6) % 2 == 1 for i in range(24)]
+        bufs = [outs(1, full) for full in kinds]  # (allocated before: the calls queue back to back)
+        tickets = [eng.search_async(pf[i % 4:i % 4 + 1], costs=full, best=True, out=bufs[i])
+                   for i, full in enumerate(kinds)]
+        outs_ = [eng.wait(t) for t in tickets]
         s0 = eng.host_stats()
-        assert s0["merged_calls"] >= 1, s0
-        for i, (full, o) in enumerate(zip(kinds, outs)):
+        assert s0["merged_calls"] >= 2 and s0["launches"] < s0["calls"], s0
+        for i, (full, o) in enumerate(zip(kinds, outs_)):
             j = i % 4
             assert np.array_equal(o["best_mode"][0], want["best_mode"][j]), (i, full)
             assert np.array_equal(o["best_cost"][0], want["best_cost"][j]), (i, full)
             if full:
                 assert np.array_equal(o["cost"][0], want["cost"][j]), i
-        # the flusher thread
-        t4 = eng.search_async(pf, costs=False, best=True)   # 4 frames of a 8-frame slot: launched
-        t1 = eng.search_async(pf[2:3], costs=False, best=True)  # busy: opens a chunk
-        time.sleep(0.5)
-        s1 = eng.host_stats()
-        assert s1["merged_launches"] == s0["merged_launches"] + 1, (s0, s1)
+        # an open chunk with the GPU idle: launched by mip_flush, or by the next call
+        b4, b1, b1b, b1c = outs(4, False), outs(1, False), outs(1, False), outs(1, False)
+        t4 = eng.search_async(pf, costs=False, best=True, out=b4)  # 4 frames of an 8-frame slot: launched
+        t1 = eng.search_async(pf[2:3], costs=False, best=True, out=b1)  # busy: opens a chunk
+        s_open = eng.host_stats()
+        time.sleep(0.2)  # (the 4-frame search completes; the chunk stays open)
+        assert eng.host_stats()["merged_launches"] == s_open["merged_launches"] == s0["merged_launches"]
+        eng.flush()
+        assert eng.host_stats()["merged_launches"] == s0["merged_launches"] + 1
         o4, o1 = eng.wait(t4), eng.wait(t1)
         assert np.array_equal(o4["best_mode"], want["best_mode"]) and np.array_equal(o1["best_cost"][0], want["best_cost"][2])
+        t4 = eng.search_async(pf, costs=False, best=True, out=b4)
+        t1 = eng.search_async(pf[1:2], costs=False, best=True, out=b1b)  # opens
+        time.sleep(0.2)
+        t2 = eng.search_async(pf[3:4], costs=False, best=True, out=b1c)  # finds the GPU idle: t1's chunk goes
+        assert eng.host_stats()["merged_launches"] == s0["merged_launches"] + 2
+        o4, o1, o2 = eng.wait(t4), eng.wait(t1), eng.wait(t2)
+        assert np.array_equal(o4["best_cost"], want["best_cost"])
+        assert np.array_equal(o1["best_mode"][0], want["best_mode"][1]) and np.array_equal(o2["best_mode"][0], want["best_mode"][3])

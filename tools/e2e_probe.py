@@ -97,7 +97,7 @@ def run(case, W, H, calls, reps, torch_after=None, device_first=0, sync=False):
             o = {"cost": alloc((F, eng.costs_per_frame), np.int32)}
             kw = dict(out=o)
         eng.search(frames, **kw)
-        rates, enq, wt = [], [], []
+        rates, enq, wt, call_us = [], [], [], []
         for _ in range(reps):
             t0 = time.perf_counter()
             if sync:  # synchronous calls one after the other (mip_search_frames)
@@ -106,7 +106,11 @@ def run(case, W, H, calls, reps, torch_after=None, device_first=0, sync=False):
                 tickets = []
                 t1 = t2 = time.perf_counter()
             else:
-                tickets = [eng.search_async(frames, **kw) for _ in range(calls)]
+                tickets, tc = [], [t0]
+                for _ in range(calls):
+                    tickets.append(eng.search_async(frames, **kw))
+                    tc.append(time.perf_counter())
+                call_us = [round(1e6 * (b - a), 1) for a, b in zip(tc, tc[1:])]
                 t1 = time.perf_counter()
                 eng.wait(tickets[-1])
                 t2 = time.perf_counter()
@@ -118,7 +122,7 @@ def run(case, W, H, calls, reps, torch_after=None, device_first=0, sync=False):
     return {"case": case, "hip_runtime": hip_runtimes(), "frames_per_call": F, "out": out, "host": host, "filter": flt, "kernel_idx": kidx,
             "max_batch": mb, "calls": calls, "sync": sync, "fps": round(float(np.median(rates)), 1),
             "fps_all": [round(r, 1) for r in rates], "enqueue_ms": [round(x, 3) for x in enq],
-            "wait_ms": [round(x, 3) for x in wt], "host_stats": stats}
+            "wait_ms": [round(x, 3) for x in wt], "host_stats": stats, "last_round_call_us": call_us}
 
 
 def main():

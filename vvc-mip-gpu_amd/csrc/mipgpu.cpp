@@ -7,8 +7,8 @@
 #include <algorithm>
 #include <functional>
 #include <atomic>
+#include <chrono>
 #include <cmath>
-#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -16,7 +16,6 @@
 #include <map>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "mip_kernels.h"
@@ -40,9 +39,29 @@ int fail(const char *fmt, ...) {
   return -1;
 }
 
+// MIPGPU_SLOW_CALLS=MS (diagnostic): every HIP call made through HIP_TRY / SLOW_CALL that
+// blocks the calling thread longer than MS milliseconds is reported on stderr.
+double slow_call_ms() {
+  static const double v = getenv("MIPGPU_SLOW_CALLS") ? atof(getenv("MIPGPU_SLOW_CALLS")) : 0.0;
+  return v;
+}
+struct SlowCall {
+  const char *what;
+  std::chrono::steady_clock::time_point t0;
+  explicit SlowCall(const char *w) : what(w) {
+    if (slow_call_ms() > 0) t0 = std::chrono::steady_clock::now();
+  }
+  ~SlowCall() {
+    if (slow_call_ms() <= 0) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > slow_call_ms()) fprintf(stderr, "mipgpu slow call: %.3f ms %s\n", ms, what);
+  }
+};
+#define SLOW_CALL(expr) ([&] { SlowCall _sc(#expr); return (expr); }())
+
 #define HIP_TRY(expr)                                                              \
   do {                                                                             \
-    hipError_t _e = (expr);                                                        \
+    hipError_t _e = SLOW_CALL(expr);                                               \
     if (_e != hipSuccess) return fail("%s: %s", #expr, hipGetErrorString(_e));     \
   } while (0)
 
@@ -622,10 +641,13 @@ struct mip_engine {
   // (open_chunk / flush_open).  One-frame launches run at 0.177 ms against 0.13 ms per frame
   // in 4-frame launches (profiles/r05_small_batch_final.jsonl), so per-frame callers (the
   // reference's loop, main.cpp:678-1241) queueing calls get the multi-frame rate.  The chunk
-  // is launched when it is full (slot frames or kMergeCalls calls), when a call that cannot
-  // join it arrives, at any mip_wait or synchronous call, before any device-API work of the
-  // engine, and -- by the engine's flusher thread -- as soon as the search launched before
-  // it has completed, so a call never waits for later calls.  MIPGPU_MERGE=0 (A/B knob): off.
+  // is launched when it is full (merge_cap frames or kMergeCalls calls), when a call that
+  // cannot join it arrives, when the next call finds the search launched before it completed
+  // (the GPU would idle), at any mip_wait / mip_flush / synchronous call, and before any
+  // device-API work of the engine.  (A first version also had a flusher thread that waited
+  // for that search with hipEventSynchronize: beside the caller's submissions it made 8 queued
+  // calls erratic, 2600-3000 frames/s against 5430 without it, profiles/r06_merge_rates.txt --
+  // so there is none.)  MIPGPU_MERGE=0 (A/B knob): off.
   static constexpr int kMergeCalls = 32;
   struct Member {
     uint64_t call;
@@ -636,22 +658,20 @@ struct mip_engine {
   struct OpenChunk {
     bool active = false;
     uint64_t k = 0;       // chunk sequence number (slot k % hp_slots)
-    uint64_t serial = 0;  // counts opened chunks (the flusher's "still the same chunk?")
     int nb = 0;           // frames so far
+    int cap = 0;          // frames it may take (merge_cap)
     unsigned sig = 0;     // outputs and reference source of its calls (merge_sig)
     std::vector<Member> members;
   } open;
   int last_slot = -1;  // slot of the last launched host-pipeline chunk (its slot_comp event)
+  int last_frames = 0;  // frames of the last launched host-pipeline chunk (merge_cap)
   uint64_t stat_launches = 0, stat_merged_calls = 0, stat_merged_launches = 0;  // mip_host_stats
   // per-frame status pointers of merged launches ([kCallRing][hp_cap], page-locked, mapped;
   // row (first call - 1) % kCallRing), SearchArgs::frame_status
   uint32_t **h_frame_status = nullptr, **d_frame_status = nullptr;
-  // Every public entry point that uses the engine holds `mu` (the flusher thread shares the
-  // engine's streams and state).
+  // Every public entry point that uses the engine holds `mu`: an engine is used by one thread
+  // at a time (include/mipgpu.h); calls from several threads are serialised, not undefined.
   std::recursive_mutex mu;
-  std::condition_variable_any flush_cv;
-  std::thread flusher;
-  bool flusher_stop = false;
 };
 
 namespace {
@@ -898,14 +918,11 @@ int mip_cu_position(int shape, int cu, int *x, int *y) {
 
 int mip_engine_destroy(mip_engine *e) {
   if (!e) return 0;
-  {  // the open chunk is launched (its calls were accepted), then the flusher stops
+  {  // the open chunk is launched (its calls were accepted)
     std::lock_guard<std::recursive_mutex> lk(e->mu);
     (void)hipSetDevice(e->device);
     (void)flush_open(e);
-    e->flusher_stop = true;
   }
-  e->flush_cv.notify_all();
-  if (e->flusher.joinable()) e->flusher.join();
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
@@ -1330,7 +1347,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const bool last = !(alt && e->nfixup[map]) && !engine_refs && !timing &&
                     (decisions_only ? defer_split != nullptr : !(d_best || d_best_cost)) && ext_done_enabled();
   hipEvent_t stop = done && last ? *done : nullptr;
-  const hipError_t le = mipgpu::launch_search(a, nframes, alt, resident, work.wide, s, stop);
+  const hipError_t le = SLOW_CALL(mipgpu::launch_search(a, nframes, alt, resident, work.wide, s, stop));
   if (le == hipSuccess && stop) *done = nullptr;
   if (le != hipSuccess) {
     ring.failed(slot);  // the pair is cleared before its next use
@@ -1422,8 +1439,8 @@ static int drain_trace(mip_engine *e, int sl) {
 enum : unsigned { kSigCost = 1, kSigSad = 2, kSigSatd = 4, kSigBestMode = 8, kSigBestCost = 16, kSigRefs = 32, kSigDec = 64 };
 
 // MIPGPU_MERGE (A/B / test knob): 0 = every call launches on its own; "hold" = small calls
-// open a chunk even into an idle pipeline and the flusher thread never launches it (only the
-// other triggers do: deterministic merges for tests).
+// open a chunk even into an idle pipeline and only a full chunk, an incompatible call, a wait
+// or a device-API call launch it (deterministic merges for tests).
 static int merge_mode() {
   const char *e = getenv("MIPGPU_MERGE");
   if (e && *e == '0') return 0;
@@ -1478,6 +1495,7 @@ static int flush_open(mip_engine *e) {
       return -1;
     if (comp_done) HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     e->last_slot = sl;
+    e->last_frames = nb;
     e->stat_launches++;
     e->stat_merged_launches++;
     e->stat_merged_calls += o.members.size();
@@ -1511,28 +1529,15 @@ static int flush_open(mip_engine *e) {
   return rc;
 }
 
-// The engine's flusher thread: launches an open chunk as soon as the search launched before
-// it has completed (a merged call never waits for later calls; calls that arrive meanwhile
-// join the chunk).  Started with the first open chunk; stopped by mip_engine_destroy.
-static void flusher_loop(mip_engine *e) {
-  (void)hipSetDevice(e->device);
-  (void)mipgpu::bind_current_thread(e->place);
-  std::unique_lock<std::recursive_mutex> lk(e->mu);
-  uint64_t seen = 0;
-  for (;;) {
-    e->flush_cv.wait(lk, [&] { return e->flusher_stop || (e->open.active && e->open.serial != seen); });
-    if (e->flusher_stop) return;
-    const uint64_t serial = seen = e->open.serial;
-    if (e->last_slot >= 0) {
-      // (the event may be recorded again meanwhile, for a later chunk: then the wait only ends
-      // later -- by then the open chunk has been launched by its owner's calls)
-      const hipEvent_t ev = e->slot_comp[e->last_slot];
-      lk.unlock();
-      (void)hipEventSynchronize(ev);
-      lk.lock();
-    }
-    if (e->open.active && e->open.serial == serial) (void)flush_open(e);
-  }
+// Frames an open chunk may take: its search can start only when all of its frames are
+// uploaded, and the uploads run during the search launched before it -- one 1080p frame
+// uploads in ~80 us, a launch of n frames searches in ~130 n + 47 us --
+// so a chunk after one of n frames takes at most 1.625 n + 0.6 frames (1, 2, 3, 5, 8, 13, ...:
+// a chunk of a whole slot right after a one-frame launch left the GPU idle for six uploads).
+// MIPGPU_MERGE=hold: up to a slot.
+static int merge_cap(const mip_engine *e) {
+  if (merge_mode() == 2) return e->hp_cap;
+  return std::max(2, std::min(e->hp_cap, (13 * std::max(1, e->last_frames) + 5) / 8));
 }
 
 // Add a call to the open chunk (opening one if there is none): its frames (and caller
@@ -1550,14 +1555,12 @@ static int merge_call(mip_engine *e, const uint16_t *frames, const uint16_t *ref
     o.k = e->host_chunks++;
     const int sl = (int)(o.k % e->hp_slots);
     o.active = true;
-    o.serial++;
     o.nb = 0;
+    o.cap = merge_cap(e);
     o.sig = sig;
     o.members.clear();
     // the slot's previous chunk is over once its downloads are (as search_frames_chunks)
     if (o.k >= (uint64_t)e->hp_slots) HIP_TRY(hipStreamWaitEvent(up, e->slot_down[sl], 0));
-    if (!e->flusher.joinable() && merge_mode() != 2) e->flusher = std::thread(flusher_loop, e);
-    e->flush_cv.notify_all();
   }
   const size_t f = (size_t)(o.k % e->hp_slots) * e->hp_cap + o.nb;
   HIP_TRY(hipMemcpyAsync(e->d_frames + f * fs, frames, nframes * fs * 2, hipMemcpyHostToDevice, up));
@@ -1578,6 +1581,13 @@ static int search_frames_call(mip_engine *e, const uint16_t *frames, const uint1
   if ((sad_out || satd_out) && !e->opts.want_sad_satd) return fail("engine created without want_sad_satd");
   HIP_TRY(hipSetDevice(e->device));
   const uint64_t next = e->host_calls + 1;
+  // MIPGPU_MAX_INFLIGHT=D (A/B knob): call `next` waits on the host until call next - D has
+  // completed (bounds the commands queued in the HIP runtime).
+  if (const char *mi = getenv("MIPGPU_MAX_INFLIGHT"); mi && atoi(mi) > 0 && next > (uint64_t)atoi(mi)) {
+    const uint64_t c = next - (uint64_t)atoi(mi);
+    if (e->open.active && e->open.members.front().call <= c && flush_open(e) != 0) return -1;
+    HIP_TRY(hipEventSynchronize(e->call_done[(c - 1) % mip_engine::kCallRing]));
+  }
   // call `next` marks status set (next - 1) % kCallRing: the call that used it before (more
   // than kCallRing calls in flight) must have completed and been harvested first
   if (next > (uint64_t)mip_engine::kCallRing && e->status_harvested < next - mip_engine::kCallRing) {
@@ -1602,13 +1612,18 @@ static int search_frames_call(mip_engine *e, const uint16_t *frames, const uint1
     const bool small = pinned && mode && !e->trace && nframes < e->hp_cap;
     mip_engine::OpenChunk &o = e->open;
     bool join = false;
+    // the search launched before the open chunk has completed: the GPU would idle -- launch
+    // the chunk now (this call then opens the next one)
+    if (o.active && mode == 1 && e->last_slot >= 0 &&
+        SLOW_CALL(hipEventQuery(e->slot_comp[e->last_slot])) == hipSuccess && flush_open(e) != 0)
+      return -1;
     if (o.active) {
-      join = small && o.sig == sig && o.nb + nframes <= e->hp_cap && (int)o.members.size() < mip_engine::kMergeCalls;
+      join = small && o.sig == sig && o.nb + nframes <= o.cap && (int)o.members.size() < mip_engine::kMergeCalls;
       if (!join && flush_open(e) != 0) return -1;
     }
-    if (!o.active && small && !sync &&
-               (mode == 2 || (e->host_calls > 0 && hipEventQuery(e->call_done[(e->host_calls - 1) %
-                                                                              mip_engine::kCallRing]) == hipErrorNotReady))) {
+    if (!o.active && small && !sync && nframes <= merge_cap(e) &&
+               (mode == 2 || (e->host_calls > 0 && SLOW_CALL(hipEventQuery(e->call_done[(e->host_calls - 1) %
+                                                                              mip_engine::kCallRing])) == hipErrorNotReady))) {
       join = true;  // the pipeline is busy: open a chunk
     }
     if (join) {
@@ -1617,7 +1632,7 @@ static int search_frames_call(mip_engine *e, const uint16_t *frames, const uint1
         return -1;
       *ticket = ++e->host_calls;
       e->host_pending = true;
-      if ((o.nb >= e->hp_cap || (int)o.members.size() >= mip_engine::kMergeCalls || sync) && flush_open(e) != 0)
+      if ((o.nb >= o.cap || (int)o.members.size() >= mip_engine::kMergeCalls || sync) && flush_open(e) != 0)
         return -1;
       return 0;
     }
@@ -1691,7 +1706,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
   // others keep whole-slot chunks (the overlap comes from the neighbouring calls, and larger
   // launches are more efficient).  sb only shrinks below.
   const bool idle = e->host_calls == 0 ||
-                    hipEventQuery(e->call_done[(e->host_calls - 1) % mip_engine::kCallRing]) == hipSuccess;
+                    SLOW_CALL(hipEventQuery(e->call_done[(e->host_calls - 1) % mip_engine::kCallRing])) == hipSuccess;
   int sb = mipgpu::call_chunk_cap(nframes, slot_cap, nslots, idle);
   // Full tables to the host (PCIe-bound): chunks of at most ~1 GiB of downloads, so the
   // first download starts early and, for pageable outputs, the bounce ring's copy-out keeps
@@ -1840,6 +1855,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
       return -1;
     if (comp_done) HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     e->last_slot = sl;
+    e->last_frames = nb;
     e->stat_launches++;
     HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));  // (also without outputs: slot_down ends the chunk)
     if (defer) HIP_TRY(mipgpu::launch_dec_split(split, nb, false, down));
@@ -1934,6 +1950,13 @@ int mip_pop_times(mip_engine *e, double *upload_ms, double *filter_ms, int max, 
   e->tr_times.erase(e->tr_times.begin(), e->tr_times.begin() + k);
   *n = k;
   return 0;
+}
+
+int mip_flush(mip_engine *e) {
+  if (!e) return fail("engine is NULL");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->device));
+  return flush_open(e);
 }
 
 int mip_host_stats(mip_engine *e, uint64_t *out, int n) {

@@ -121,6 +121,7 @@ def library():
         "mip_search_frames": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp]),
         "mip_search_frames_async": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "mip_wait": (ip, [vp, ctypes.c_uint64]),
+        "mip_flush": (ip, [vp]),
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
         "mip_search_device_range": (ip, [vp, vp, vp, ip, ip, ip, vp, vp, vp, vp]),
         "mip_check_input": (ip, [vp, vp]),
@@ -343,6 +344,12 @@ class MipEngine:
         with self._lock:
             _check(library().mip_host_stats(self._h, out, 4))
         return dict(zip(("calls", "launches", "merged_calls", "merged_launches"), (int(v) for v in out)))
+
+    def flush(self):
+        """Launch the engine's open (merged) chunk now (mip_flush): queued small calls are
+        otherwise launched by the next call, a wait, or when the chunk is full."""
+        with self._lock:
+            _check(library().mip_flush(self._h))
 
     def filter_frames(self, frames, filter, kernel_idx=0):
         f = self._frames(frames)
