@@ -3,9 +3,9 @@
 # with the HIP runtime's direct dispatch (default) and without (AMD_DIRECT_DISPATCH=0).
 set -uo pipefail
 cd "$(dirname "$0")/../../.."
-O=gpurun_out/r06k; mkdir -p $O
+O=gpurun_out/${OUTTAG:-r06k}; mkdir -p $O
 : > $O/merge_rates.jsonl
-for dd in 1 0; do
+for dd in ${DDS:-1 0}; do
   for m in 1 0; do
     for calls in 8 32; do
       AMD_DIRECT_DISPATCH=$dd MIPGPU_MERGE=$m timeout -k 10 200 python -u tools/e2e_probe.py --reps 15 --calls $calls 1:dec:pinned:mb=4 1:dec:pinned:mb=8 1:full:pinned:mb=4 > $O/t.jsonl 2> $O/t.err || { tail $O/t.err; exit 1; }
