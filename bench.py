@@ -290,10 +290,38 @@ def cpu_baseline(width, height, seed, budget_s=10.0):
             "%dx%d frames/s" % (width, height), "cores": threads, "kind": "port",
             "configs0": "BASELINE configs[0] names the reference's OpenCL kernels on the host CPU's OpenCL device; "
                         "this image has no CPU OpenCL device (SURVEY.md 8c: the AMD ICD lists 0 CPU devices, no "
-                        "PoCL), so that run is not possible here -- this figure is the C port of the reference "
-                        "pipeline (oracle/mip_oracle.c), not the reference itself",
+                        "PoCL), so this figure is the C port of the reference pipeline (oracle/mip_oracle.c); the "
+                        "reference's own kernels compiled for the CPU are `reference_kernels`",
             "sample": "%d synthetic %dx%d frames (all CTUs, full search, same generator as the GPU run) through "
                       "the C oracle oracle/mip_oracle.c, OpenMP %d threads, %.1f s" % (n, width, height, threads, dt)}
+
+
+def reference_kernels_cpu(width, height, seed):
+    """BASELINE configs[0] / SURVEY 8d C1: the reference's own kernels (/root/reference's
+    intra.cl compiled by clang for the host CPU with oracle/ref/cl_cpu_shim.cl's builtins --
+    oracle/_ref/ref_cpu_runner, built in the container) on one 1080p frame, original
+    references, every work-group, on the host cores; None when the runner was not built."""
+    runner = os.path.join(REPO, "oracle", "_ref", "ref_cpu_runner")
+    if not os.path.exists(runner):
+        return None
+    workers = min(16, os.cpu_count() or 1)
+    try:
+        out = subprocess.run([runner, "--libs", os.path.join(REPO, "oracle", "_ref"), "--width", str(width),
+                              "--height", str(height), "--synth", "0:%x" % seed, "--workers", str(workers)],
+                             capture_output=True, timeout=300, check=True).stdout.decode()
+        d = json.loads(out.strip().splitlines()[-1])
+    except Exception as exc:  # informative only
+        return {"error": str(exc)[:200]}
+    return {"value": round(d["frames_per_s"], 5),
+            "unit": "1080p frames/s" if (width, height) == (1920, 1080) else "%dx%d frames/s" % (width, height),
+            "cores": workers, "kind": "reference",
+            "kernel_s_per_frame": d["kernel_s"], "wall_s_per_frame": round(d["wall_s_per_frame"], 3),
+            "sample": "one synthetic %dx%d frame, original references (BASELINE configs[0]), every work-group of "
+                      "initBoundaries, MIP_ReducedPred and the three upsampleDistortion builds" % (width, height),
+            "note": "the reference's own intra.cl kernels compiled by clang for x86-64 (oracle/Makefile ref-cpu) with "
+                    "the OpenCL builtins of oracle/ref/cl_cpu_shim.cl, work-groups over %d worker processes, "
+                    "work-items as fibers (oracle/ref/ref_cpu_runner.cpp); its tables hash like the golden fixtures "
+                    "the same kernels made on the MI355X (tests/test_ref_cpu.py).  A baseline, not a target" % workers}
 
 
 def reference_kernel_trace(cmd, frames, reps):
@@ -640,6 +668,9 @@ def main():
         if world == 1:
             if not args.no_cpu_baseline:
                 res["cpu_baseline"] = cpu_baseline(W, H, args.seed)
+                rk = reference_kernels_cpu(W, H, args.seed)
+                if rk is not None:
+                    res["cpu_baseline"]["reference_kernels"] = rk
         if world == 1 and not args.no_end_to_end:
             # Host-buffer path incl. PCIe (informative, never `value`): page-locked buffers
             # (mip_host_alloc; transfers overlap the next chunk's search) and pageable ones.
