@@ -165,6 +165,14 @@ int mip_wait(mip_engine *e, uint64_t ticket);
 /* Launch the engine's open (merged) chunk now, if any (see mip_search_frames_async); no wait. */
 int mip_flush(mip_engine *e);
 
+/* Device block cache (ABI 7).  Freeing a large device allocation halves every later host <->
+ * device copy of the process on the MI355X platform (profiles/r06_free_repro.txt), so
+ * mip_engine_destroy parks its buffers of >= 16 MB in a process-wide cache that later engines
+ * on the same device reuse (the smallest block that fits).  mip_device_cache reports the
+ * parked bytes of `device` and the blocks reused so far; release = 1 frees the parked blocks
+ * first (hipFree: the copies of the process may slow down afterwards). */
+int mip_device_cache(int device, int release, uint64_t *idle_bytes, uint64_t *reused_blocks);
+
 /* Device-resident variant (inputs already in HBM; all pointers are device pointers,
  * `stream` is a hipStream_t; NULL means the default (null) stream, as in HIP).
  * Asynchronous on `stream`.

@@ -924,3 +924,31 @@ def test_merged_launches_1080p_default_policy(gpu_available):
         o4, o1, o2 = eng.wait(t4), eng.wait(t1), eng.wait(t2)
         assert np.array_equal(o4["best_cost"], want["best_cost"])
         assert np.array_equal(o1["best_mode"][0], want["best_mode"][1]) and np.array_equal(o2["best_mode"][0], want["best_mode"][3])
+
+
+def test_engine_churn_reuses_parked_device_blocks(gpu_available):
+    """Device block cache (mipgpu.cpp dev_malloc / dev_free): a destroyed engine's large buffers
+    are parked, not freed (a large hipFree halves the process's later transfer rate,
+    profiles/r06_free_repro.txt), and the next engine on the device takes them -- whose
+    results stay exact although its buffers hold the previous engine's data (every output is
+    written, the split accumulator re-initialised)."""
+    from mipgpu import device_cache, pinned_empty
+    W, H = 1920, 1080
+    frames = synth_frames(W, H, 2, 0xC4C, 0)
+    with MipEngine(W, H, max_batch=16) as big:
+        want = big.search(frames, best=True)
+        dec0 = big.search(frames, costs=False, best=True)
+    assert np.array_equal(dec0["best_cost"], want["best_cost"])
+    c0 = device_cache(0)
+    assert c0["idle_bytes"] >= 16 * 135 * 97840 * 4 // 4, c0  # (at least the cost table's slots)
+    pf = pinned_empty(frames.shape, np.uint16)
+    pf[:] = frames
+    with MipEngine(W, H, max_batch=2) as eng:
+        c1 = device_cache(0)
+        assert c1["reused_blocks"] > c0["reused_blocks"] and c1["idle_bytes"] < c0["idle_bytes"], (c0, c1)
+        full = eng.search(pf, best=True)
+        dec = eng.search(pf, costs=False, best=True)
+    for k in ("cost", "best_mode", "best_cost"):
+        assert np.array_equal(full[k], want[k]), k
+    assert np.array_equal(dec["best_mode"], want["best_mode"]) and np.array_equal(dec["best_cost"], want["best_cost"])
+    assert np.array_equal(want["cost"][1], O.search(frames[1]))

@@ -56,7 +56,12 @@ def big_engine():
         pass
 
 
-print(json.dumps({"phase": "start", "fps": rate()}), flush=True)
+def cache():
+    from mipgpu import device_cache
+    return device_cache(0)
+
+
+print(json.dumps({"phase": "start", "fps": rate(), "device_cache": cache()}), flush=True)
 if os.environ.get("RAW"):  # a plain 20 GB hipMalloc / hipFree in the engine's HIP runtime
     import ctypes
     from mipgpu import hip_runtimes, library
@@ -80,9 +85,9 @@ if os.environ.get("RAW"):  # a plain 20 GB hipMalloc / hipFree in the engine's H
 big_host()
 print(json.dumps({"phase": "after 6.8 GB page-locked host", "fps": rate()}), flush=True)
 big_engine()
-print(json.dumps({"phase": "after a max_batch-384 engine", "fps": rate()}), flush=True)
+print(json.dumps({"phase": "after a max_batch-384 engine", "fps": rate(), "device_cache": cache()}), flush=True)
 print(json.dumps({"phase": "again", "fps": rate()}), flush=True)
-print(json.dumps({"phase": "decisions only", "fps": rate(dec=True)}), flush=True)
+print(json.dumps({"phase": "decisions only", "fps": rate(dec=True), "device_cache": cache()}), flush=True)
 if os.environ.get("DEVICE"):  # device-API search time of the same frame (torch)
     import torch
     d = torch.from_numpy(synth_frames(W, H, 1, 0x1080, 0).astype(np.int16)).cuda()

@@ -840,6 +840,83 @@ static int wait_refs_readers(mip_engine *e) {
 // Launch the engine's open (merged) chunk, if any (defined with the host pipeline below).
 static int flush_open(mip_engine *e);
 
+// Device block cache (round 6).  Freeing a large device allocation halves every later
+// host <-> device copy of the process on this platform -- 56.4 -> 28.7 GB/s, SDMA and blit
+// copies alike, old and new buffers, whatever the NUMA placement or the number of streams
+// (tools/free_repro.hip, profiles/r06_free_repro.txt: a standalone HIP program, no engine) --
+// until some later page-locked allocation churn restores it, on some boxes only.  Engines are
+// created and destroyed by serving processes (a resolution change), so engine buffers of at
+// least kCacheMin bytes are not freed: mip_engine_destroy parks them in a process-wide cache,
+// and later engines on the same device take the smallest parked block that fits (blocks are
+// not split: the process holds at most its largest engine set).  hipMalloc failing for lack of
+// memory releases the device's parked blocks and retries; mip_device_cache(device, 1, ...)
+// releases them explicitly.  MIPGPU_DEVICE_CACHE=0 (A/B knob): plain hipMalloc / hipFree.
+namespace {
+constexpr size_t kCacheMin = 16u << 20;
+struct BlockCache {
+  std::mutex mu;
+  std::map<void *, std::pair<int, size_t>> live;      // blocks handed out: (device, bytes)
+  std::multimap<std::pair<int, size_t>, void *> idle;  // parked blocks by (device, bytes)
+  uint64_t reused = 0;
+};
+BlockCache &block_cache() {
+  static BlockCache *c = new BlockCache();  // (never destroyed: no hipFree at process exit)
+  return *c;
+}
+bool device_cache_enabled() {
+  const char *e = getenv("MIPGPU_DEVICE_CACHE");
+  return !(e && *e == '0');
+}
+// hipMalloc on `device` (the current device) through the cache.
+hipError_t dev_malloc(int device, void **p, size_t bytes) {
+  if (bytes < kCacheMin || !device_cache_enabled()) return hipMalloc(p, bytes);
+  BlockCache &c = block_cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.idle.lower_bound({device, bytes});
+    if (it != c.idle.end() && it->first.first == device) {
+      *p = it->second;
+      c.live[*p] = it->first;
+      c.idle.erase(it);
+      c.reused++;
+      return hipSuccess;
+    }
+  }
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {  // release the parked blocks, retry
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto it = c.idle.begin(); it != c.idle.end();)
+      if (it->first.first == device) {
+        (void)hipFree(it->second);
+        it = c.idle.erase(it);
+      } else {
+        ++it;
+      }
+    e = hipMalloc(p, bytes);
+  }
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.live[*p] = {device, bytes};
+  }
+  return e;
+}
+void dev_free(void *p) {
+  if (!p) return;
+  BlockCache &c = block_cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it != c.live.end()) {
+      c.idle.insert({it->second, p});
+      c.live.erase(it);
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+}  // namespace
+
 // NUMA placement of a device (numa_place.h; none when the bus id or its node is unknown).
 static mipgpu::NumaPlace device_place(int device) {
   char bus[64] = {};
@@ -932,12 +1009,12 @@ int mip_engine_destroy(mip_engine *e) {
   for (void *p : {(void *)e->d_frames, (void *)e->d_refs, (void *)e->d_costs, (void *)e->d_sad,
                   (void *)e->d_satd, (void *)e->d_best, (void *)e->d_best_cost, (void *)e->d_split_acc,
                   (void *)e->d_tables})
-    if (p) (void)hipFree(p);
+    dev_free(p);
   for (int m = 0; m < kMaps; m++) {
-    if (e->d_ctu_var[m]) (void)hipFree(e->d_ctu_var[m]);
-    if (e->d_fixup[m]) (void)hipFree(e->d_fixup[m]);
+    dev_free(e->d_ctu_var[m]);
+    dev_free(e->d_fixup[m]);
   }
-  if (e->d_queue) (void)hipFree(e->d_queue);
+  dev_free(e->d_queue);
   if (e->h_status) (void)hipHostFree(e->h_status);
   if (e->h_frame_status) (void)hipHostFree(e->h_frame_status);
   for (hipEvent_t ev : e->queue_done)
@@ -955,7 +1032,7 @@ int mip_engine_destroy(mip_engine *e) {
     for (void *p : {(void *)w.d_tasks, (void *)w.d_jobs, (void *)w.d_lists, (void *)w.d_fill, (void *)w.d_fill_begin,
                     (void *)w.d_dfill, (void *)w.d_dfill_begin, (void *)w.d_split, (void *)w.d_split_begin,
                     (void *)w.d_order})
-      if (p) (void)hipFree(p);
+      dev_free(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
   if (e->stream3) (void)hipStreamDestroy(e->stream3);
@@ -1013,7 +1090,7 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
   auto cleanup = [&](int rc) { mip_engine_destroy(e); return rc; };
 #define ALLOC(ptr, bytes)                                                               \
   do {                                                                                  \
-    hipError_t _e = hipMalloc((void **)&(ptr), (bytes));                                \
+    hipError_t _e = dev_malloc(device, (void **)&(ptr), (bytes));                       \
     if (_e != hipSuccess) return cleanup(fail("hipMalloc(%zu): %s", (size_t)(bytes), hipGetErrorString(_e))); \
   } while (0)
   {
@@ -1055,7 +1132,7 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
       if (hipEventCreateWithFlags(ev, slot_flags) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
   for (hipEvent_t &ev : e->call_done)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return cleanup(fail("hipEventCreate failed"));
-  ALLOC(e->d_frames, fs * nb * 2);
+  ALLOC(e->d_frames, fs * nb * 2);  // (through the device block cache, dev_malloc)
   if (o.filter != MIP_FILTER_NONE) ALLOC(e->d_refs, fs * nb * 2);
   ALLOC(e->d_costs, ncost * 4);
   if (o.want_sad_satd) {
@@ -1549,7 +1626,7 @@ static int merge_call(mip_engine *e, const uint16_t *frames, const uint16_t *ref
   const hipStream_t up = e->stream2;
   if (!o.active) {
     if ((refs || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
-      HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
+      HIP_TRY(dev_malloc(e->device, (void **)&e->d_refs, fs * e->hp_frames * 2));
     if (wait_refs_readers(e) != 0) return -1;
     e->refs_pending = false;
     o.k = e->host_chunks++;
@@ -1678,7 +1755,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
                                 int32_t *satd_out, uint64_t call, bool sync) {
   const size_t fs = (size_t)e->width * e->height;
   if ((refs_or_null || e->opts.filter != MIP_FILTER_NONE) && !e->d_refs)
-    HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
+    HIP_TRY(dev_malloc(e->device, (void **)&e->d_refs, fs * e->hp_frames * 2));
   if (wait_refs_readers(e) != 0) return -1;
   e->refs_pending = false;  // the waits above order every later use of the engine streams
   const size_t cpf = (size_t)e->nctus * MIP_COSTS_PER_CTU, upf = (size_t)e->nctus * MIP_CUS_PER_CTU * e->opts.best_k;
@@ -1952,6 +2029,28 @@ int mip_pop_times(mip_engine *e, double *upload_ms, double *filter_ms, int max, 
   return 0;
 }
 
+int mip_device_cache(int device, int release, uint64_t *idle_bytes, uint64_t *reused_blocks) {
+  BlockCache &c = block_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  uint64_t idle = 0;
+  for (auto it = c.idle.begin(); it != c.idle.end();) {
+    if (it->first.first == device && release) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(device);
+      (void)hipFree(it->second);
+      (void)hipSetDevice(cur);
+      it = c.idle.erase(it);
+      continue;
+    }
+    if (it->first.first == device) idle += it->first.second;
+    ++it;
+  }
+  if (idle_bytes) *idle_bytes = idle;
+  if (reused_blocks) *reused_blocks = c.reused;
+  return 0;
+}
+
 int mip_flush(mip_engine *e) {
   if (!e) return fail("engine is NULL");
   std::lock_guard<std::recursive_mutex> lk(e->mu);
@@ -2004,7 +2103,7 @@ int mip_filter_frames(mip_engine *e, const uint16_t *frames, int nframes, int fi
   HIP_TRY(hipSetDevice(e->device));
   if (flush_open(e) != 0) return -1;
   const size_t fs = (size_t)e->width * e->height;
-  if (!e->d_refs) HIP_TRY(hipMalloc((void **)&e->d_refs, fs * e->hp_frames * 2));
+  if (!e->d_refs) HIP_TRY(dev_malloc(e->device, (void **)&e->d_refs, fs * e->hp_frames * 2));
   if (wait_refs_readers(e) != 0) return -1;
   // asynchronous host searches still in flight use d_frames / d_refs: let them finish
   HIP_TRY(hipStreamSynchronize(e->stream2));

@@ -122,6 +122,7 @@ def library():
         "mip_search_frames_async": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "mip_wait": (ip, [vp, ctypes.c_uint64]),
         "mip_flush": (ip, [vp]),
+        "mip_device_cache": (ip, [ip, ip, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "mip_search_device": (ip, [vp, vp, vp, ip, vp, vp, vp, vp, vp, vp]),
         "mip_search_device_range": (ip, [vp, vp, vp, ip, ip, ip, vp, vp, vp, vp]),
         "mip_check_input": (ip, [vp, vp]),
@@ -406,6 +407,14 @@ class MipEngine:
         return ms
 
 
+def device_cache(device=0, release=False) -> dict:
+    """The process-wide device block cache (mip_device_cache): bytes parked for `device` by
+    destroyed engines and blocks reused so far; release=True frees the parked blocks first."""
+    idle, reused = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(library().mip_device_cache(int(device), int(bool(release)), ctypes.byref(idle), ctypes.byref(reused)))
+    return {"idle_bytes": int(idle.value), "reused_blocks": int(reused.value)}
+
+
 def numa_node(device) -> int:
     """NUMA node of a GPU (mip_numa_node; -1: unknown or a one-node host)."""
     return int(library().mip_numa_node(int(device)))
@@ -451,5 +460,5 @@ def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
 
 
 __all__ = ["MipEngine", "MipError", "build_id", "source_id", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "topk_device", "library",
-           "pinned_empty", "unavailable_cus", "numa_node", "bind_thread",
+           "pinned_empty", "unavailable_cus", "numa_node", "bind_thread", "device_cache",
            "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]
