@@ -241,8 +241,17 @@ def filter_section(eng_cls, frames, W, H, B, stream, dev, steps, pmc):
     e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
-    # calibration: a device-to-device copy of the same bytes on the same stream (the rate this
-    # size reaches in practice; 384 frames are far past the last-level cache)
+    # calibration: a streaming copy of the same bytes on the same stream (mip_copy_device:
+    # 16 bytes per lane, four loads in flight -- the guide's achievable-copy form; 384 frames
+    # are far past the last-level cache); torch's copy_ beside it (round 5's calibration)
+    from mipgpu import copy_device
+    copy_device(frames, out, stream=stream)
+    e0.record(stream)
+    for _ in range(steps):
+        copy_device(frames, out, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    copy_ms = e0.elapsed_time(e1) / steps
     with torch.cuda.stream(stream):
         out.copy_(frames)
         e0.record(stream)
@@ -250,13 +259,15 @@ def filter_section(eng_cls, frames, W, H, B, stream, dev, steps, pmc):
             out.copy_(frames)
         e1.record(stream)
     torch.cuda.synchronize(dev)
-    copy_ms = e0.elapsed_time(e1) / steps
+    torch_copy_ms = e0.elapsed_time(e1) / steps
     alg = 2 * 2 * W * H * B
     res = {"kernel": "filter_kernel<2, true, false>", "filter": name, "kernel_idx": kidx, "bound": "hbm",
            "kernel_ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": alg,
            "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "copy_GBps": round(alg / (copy_ms * 1e-3) / 1e9, 1), "frac_of_copy": round(copy_ms / ms, 4),
+           "copy_kernel": "mip_copy_device (16 B per lane, 4 loads in flight)",
+           "torch_copy_GBps": round(alg / (torch_copy_ms * 1e-3) / 1e9, 1),
            "traffic": (pmc.get("filter") or {}).get("hbm_bytes_per_launch")}
     alt = eng_cls(W, H, device=dev.index, filter=name, kernel_idx=kidx, max_batch=B)
     costs = torch.empty((B, alt.costs_per_frame), dtype=torch.int32, device=dev)

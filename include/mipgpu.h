@@ -212,6 +212,11 @@ int mip_search_device_range(mip_engine *e, const uint16_t *d_frames, const uint1
 int mip_topk_device(const int32_t *d_costs, int width, int height, int nframes, int k,
                     uint8_t *d_modes, int32_t *d_costs_k, void *stream);
 
+/* Streaming device-to-device copy of `bytes` (a multiple of 16, 16-byte aligned pointers),
+ * asynchronous on `stream`: 16 bytes per lane, four loads in flight per lane -- the HBM copy
+ * rate bench.py prices the filter kernel against (no reference counterpart). */
+int mip_copy_device(const void *d_src, void *d_dst, size_t bytes, void *stream);
+
 /* Device-resident filter (asynchronous on `stream`). */
 int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int height,
                       int nframes, int filter, int kernel_idx, void *stream);

@@ -49,5 +49,21 @@ e1.record(s)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / REPS
 copy = {"ms_per_launch": round(ms, 4), "GB/s": round(4 * W * H * B / (ms * 1e-3) / 1e9, 1)}
+try:  # the library's streaming copy (16 B per lane, 4 loads in flight): bench.py's calibration
+    from mipgpu import copy_device
+    for _ in range(3):
+        copy_device(frames, out, stream=s)
+    e0.record(s)
+    for _ in range(REPS):
+        copy_device(frames, out, stream=s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / REPS
+    copy = {"torch_copy": copy, "ms_per_launch": round(ms, 4), "GB/s": round(4 * W * H * B / (ms * 1e-3) / 1e9, 1),
+            "kernel": "mip_copy_device"}
+except ImportError:
+    pass
+for v in res.values():
+    v["frac_of_copy"] = round(copy["ms_per_launch"] / v["ms_per_launch"], 3)
 print(json.dumps({"workload": "%dx%d x %d frames, kernel_idx %d" % (W, H, B, KIDX), "filters": res,
                   "copy_calibration": copy}, indent=1))

@@ -24,6 +24,8 @@
 // exactly the reference's own fp32 division sequence (frexp, v_rcp_f32, v_mul, v_ldexp:
 // the AMD OpenCL lowering of '/', read from the reference's code objects), since scaling
 // by a power of two commutes with the multiply's rounding.
+#include <algorithm>
+
 #include "mip_kernels.h"
 #include "mip_tables.h"
 
@@ -33,7 +35,17 @@ namespace {
 typedef short s2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u2 __attribute__((ext_vector_type(2)));
 
-constexpr int kThreads = 128;  // per tile: thread t owns columns 4(t&31).. +3, rows 8(t>>5).. +7
+// Threads per tile: thread t owns columns 4(t&31).. +3 and 1024/NT rows from (1024/NT)(t>>5).
+// Separable filters: 64 (one wave, 16 rows per thread: each thread's horizontal passes of
+// the 2 RAD halo rows serve 16 output rows instead of 8); 2-D filters: 128 (384 x 1080p, one
+// box, two reps: separable 3 taps 0.679 -> 0.638 ms, 5 taps 0.680-0.707 -> 0.640-0.657 ms,
+// 2-D unchanged; 256 threads slower throughout; profiles/r06_filter_threads.txt).
+// MIP_FILTER_THREADS (A/B): one count for all eight.
+#ifndef MIP_FILTER_THREADS
+#define MIP_FILTER_THREADS 0
+#endif
+template <bool SEP>
+constexpr int kThreadsOf = MIP_FILTER_THREADS ? MIP_FILTER_THREADS : (SEP ? 64 : 128);
 #ifndef MIP_FILTER_TPW
 #define MIP_FILTER_TPW 1
 #endif
@@ -131,6 +143,7 @@ __device__ __forceinline__ short inner_value(const uint16_t *in, int x, int y, i
 // Returns whether this thread stored an invalid (-1) cell.
 template <int RAD, bool SEP>
 __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, int qy, int W, int H) {
+  constexpr int kThreads = kThreadsOf<SEP>;
   constexpr int TW = 128 + 2 * RAD;
   const int t = threadIdx.x % kThreads;
   bool invalid = false;
@@ -179,9 +192,10 @@ __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, i
   if ((W & 7) == 0) {
     // W % 8 == 0: a chunk of 8 columns lies entirely inside or entirely outside the frame's
     // linear extent; rows below the frame and indexes past its end read inner_value's fill
-    uint4 v[4];
+    constexpr int NC = 512 / kThreads;  // 16-byte chunks of the 32 x 128 tile per thread
+    uint4 v[NC];
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
+    for (int p = 0; p < NC; p++) {
       const int i = p * kThreads + t, r = i >> 4, k = i & 15;
       const int y = qy + r, x = qx + 8 * k;
       if (y < H && y * W + x + 8 <= W * H) {
@@ -194,7 +208,7 @@ __device__ __forceinline__ bool stage(short *tile, const uint16_t *in, int qx, i
       }
     }
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
+    for (int p = 0; p < NC; p++) {
       const int i = p * kThreads + t, r = i >> 4, k = i & 15;
       *reinterpret_cast<uint4 *>(tile + (r + RAD) * kTWP + kCO + 8 * k) = v[p];
     }
@@ -291,8 +305,10 @@ __device__ __forceinline__ int sep_scale(int x, int y, int W, int H, int full, c
 }
 
 template <int RAD, bool FLOAT, bool SEP>
-__global__ __launch_bounds__(kThreads * kTPW) void filter_kernel(FilterArgs a) {
-  constexpr int KS = 2 * RAD + 1, TH = 32 + 2 * RAD, NR = 8 + 2 * RAD;
+__global__ __launch_bounds__(kThreadsOf<SEP> * kTPW) void filter_kernel(FilterArgs a) {
+  constexpr int kThreads = kThreadsOf<SEP>, kRows = 32 * 32 / kThreads;
+  static_assert(kThreads == 64 || kThreads == 128 || kThreads == 256, "threads per tile");
+  constexpr int KS = 2 * RAD + 1, TH = 32 + 2 * RAD, NR = kRows + 2 * RAD;
   __shared__ __attribute__((aligned(16))) short tiles[kTPW][TH * kTWP];
   const int W = a.width, H = a.height;
   const int sub = kTPW > 1 ? (int)threadIdx.x / kThreads : 0;  // tile of this thread's 128-thread group
@@ -348,7 +364,7 @@ __global__ __launch_bounds__(kThreads * kTPW) void filter_kernel(FilterArgs a) {
     }
   }
 
-  const int c0 = 4 * (threadIdx.x & 31), r0 = 8 * ((threadIdx.x % kThreads) >> 5);
+  const int c0 = 4 * (threadIdx.x & 31), r0 = kRows * ((threadIdx.x % kThreads) >> 5);
   const short *rowp = tile + r0 * kTWP + kCO - 2 + c0;
   // Horizontal sums are produced one row ahead of the vertical pass that consumes them
   // (a sliding window of KS rows stays live, not all NR: fewer VGPRs, higher occupancy).
@@ -369,7 +385,7 @@ __global__ __launch_bounds__(kThreads * kTPW) void filter_kernel(FilterArgs a) {
 
   uint16_t *out = a.out + (size_t)f * W * H;
 #pragma unroll
-  for (int r = 0; r < 8; r++) {
+  for (int r = 0; r < kRows; r++) {
     const int y = qy + r0 + r;
     hpass<RAD, false>(rowp + (r + KS - 1) * kTWP, tt, h01[r + KS - 1], h23[r + KS - 1]);
     uint32_t num[4];
@@ -435,7 +451,35 @@ __global__ __launch_bounds__(kThreads * kTPW) void filter_kernel(FilterArgs a) {
   }
 }
 
+// Streaming copy (bench.py's calibration of the filter's HBM roofline, mip_copy_device): 16
+// bytes per lane, four loads in flight per lane before their stores, grid-stride over the
+// buffer -- the guide's measured achievable copy is this form (MI355X_MICROARCH.md: float4
+// copy 6.29 TB/s).
+__global__ __launch_bounds__(256) void copy_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, size_t n16) {
+  const size_t stride = (size_t)gridDim.x * 1024;
+  size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x;
+  for (; i + 768 < n16; i += stride) {
+    const uint4 v0 = src[i], v1 = src[i + 256], v2 = src[i + 512], v3 = src[i + 768];
+    dst[i] = v0;
+    dst[i + 256] = v1;
+    dst[i + 512] = v2;
+    dst[i + 768] = v3;
+  }
+  for (; i < n16; i += 256) dst[i] = src[i];
+}
+
 }  // namespace
+
+hipError_t launch_copy(const void *src, void *dst, size_t bytes, hipStream_t s) {
+  if (bytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16) return hipErrorInvalidValue;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return hipErrorInvalidValue;
+  const size_t n16 = bytes / 16, blocks = std::min<size_t>((size_t)cus * 8, (n16 + 1023) / 1024);
+  hipLaunchKernelGGL(copy_kernel, dim3((unsigned)std::max<size_t>(1, blocks)), dim3(256), 0, s,
+                     (const uint4 *)src, (uint4 *)dst, n16);
+  return hipGetLastError();
+}
 
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s) {
   const long long total = (long long)((a.width + 127) / 128) * ((a.height + 31) / 32) * a.nframes;
@@ -444,14 +488,14 @@ hipError_t launch_filter(const FilterArgs &a, hipStream_t s) {
     return hipErrorInvalidValue;  // 32-bit / 24-bit index arithmetic in the gates
   const long long units = (total + kTPW - 1) / kTPW;
   const dim3 grid((unsigned)((units + 7) / 8 * 8));
-  const dim3 block(kThreads * kTPW);
+  const dim3 sep_block(kThreadsOf<true> * kTPW), block(kThreadsOf<false> * kTPW);
   switch (a.filter) {
-    case 0: hipLaunchKernelGGL((filter_kernel<1, false, true>), grid, block, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((filter_kernel<1, true, true>), grid, block, 0, s, a); break;
+    case 0: hipLaunchKernelGGL((filter_kernel<1, false, true>), grid, sep_block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((filter_kernel<1, true, true>), grid, sep_block, 0, s, a); break;
     case 2: hipLaunchKernelGGL((filter_kernel<1, false, false>), grid, block, 0, s, a); break;
     case 3: hipLaunchKernelGGL((filter_kernel<1, true, false>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((filter_kernel<2, false, true>), grid, block, 0, s, a); break;
-    case 5: hipLaunchKernelGGL((filter_kernel<2, true, true>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((filter_kernel<2, false, true>), grid, sep_block, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((filter_kernel<2, true, true>), grid, sep_block, 0, s, a); break;
     case 6: hipLaunchKernelGGL((filter_kernel<2, false, false>), grid, block, 0, s, a); break;
     case 7: hipLaunchKernelGGL((filter_kernel<2, true, false>), grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;

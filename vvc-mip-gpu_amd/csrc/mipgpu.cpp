@@ -1296,6 +1296,12 @@ int mip_topk_device(const int32_t *d_costs, int width, int height, int nframes, 
   return 0;
 }
 
+int mip_copy_device(const void *d_src, void *d_dst, size_t bytes, void *stream) {
+  if (!d_src || !d_dst) return fail("bad copy arguments");
+  HIP_TRY(mipgpu::launch_copy(d_src, d_dst, bytes, (hipStream_t)stream));
+  return 0;
+}
+
 int mip_filter_device(const uint16_t *d_in, uint16_t *d_out, int width, int height, int nframes,
                       int filter, int kernel_idx, void *stream) {
   if (!d_in || !d_out || nframes < 1) return fail("bad filter arguments");

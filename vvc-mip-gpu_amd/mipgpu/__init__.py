@@ -128,6 +128,7 @@ def library():
         "mip_check_input": (ip, [vp, vp]),
         "mip_unavailable_cus": (ip, [ip, ip, ip, vp]),
         "mip_filter_device": (ip, [vp, vp, ip, ip, ip, ip, ip, vp]),
+        "mip_copy_device": (ip, [vp, vp, ctypes.c_size_t, vp]),
         "mip_topk_device": (ip, [vp, ip, ip, ip, ip, vp, vp, vp]),
         "mip_time_search_device": (ctypes.c_double, [vp, vp, vp, ip, vp, ip]),
         "mip_host_stats": (ip, [vp, ctypes.POINTER(ctypes.c_uint64), ip]),
@@ -450,6 +451,17 @@ def topk_device(costs, width, height, k, modes=None, costs_k=None, stream=None):
     return modes, costs_k
 
 
+def copy_device(src, dst, stream=None):
+    """Streaming device copy of tensor `src` into `dst` (mip_copy_device; same byte size)."""
+    import torch
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != n:
+        raise MipError("copy_device: sizes differ")
+    s = stream if stream is not None else torch.cuda.current_stream(src.device)
+    _check(library().mip_copy_device(_ptr(src), _ptr(dst), n, ctypes.c_void_p(s.cuda_stream)))
+    return dst
+
+
 def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
     import torch
     n, h, w = frames_in.shape
@@ -460,5 +472,5 @@ def filter_device(frames_in, frames_out, filter, kernel_idx=0, stream=None):
 
 
 __all__ = ["MipEngine", "MipError", "build_id", "source_id", "FILTERS", "FILTER_NONE", "filter_index", "filter_device", "topk_device", "library",
-           "pinned_empty", "unavailable_cus", "numa_node", "bind_thread", "device_cache",
+           "pinned_empty", "unavailable_cus", "numa_node", "bind_thread", "device_cache", "copy_device",
            "layout", "SHAPES", "COSTS_PER_CTU", "CUS_PER_CTU", "UNAVAILABLE", "num_ctus"]
