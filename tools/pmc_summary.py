@@ -17,9 +17,25 @@ for path in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection
     for (k, disp), cs in per.items():
         for c, v in cs.items():
             acc[k][c].append(v)
+
+
+def name(k):
+    """Full template name without the argument list and the anonymous-namespace tag
+    (round 5's summaries cut every name at "(anonymous namespace)": "void mipgpu::")."""
+    k = k.replace("(anonymous namespace)::", "")
+    if k.endswith(")") and "(" in k:
+        depth = 0
+        for i in range(len(k) - 1, -1, -1):  # the matching "(" of the final ")"
+            depth += k[i] == ")"
+            depth -= k[i] == "("
+            if depth == 0:
+                k = k[:i]
+                break
+    return k
+
+
 for k, cs in acc.items():
-    short = k.split("(")[0][-60:]
-    print("kernel:", short)
+    print("kernel:", name(k))
     for c in sorted(cs):
         vals = cs[c]
         print("  %-24s mean %.6g over %d dispatches" % (c, sum(vals) / len(vals), len(vals)))
