@@ -190,7 +190,7 @@ def load_pmc(width, height, frames, build):
 # Environment knobs of libmipgpu.so that change the work or the launch shape (profiling / A/B
 # tools).  A headline number is refused while any of them is set; --allow-knobs (the A/B
 # scripts) records them in the line instead.  Print-only diagnostics are harmless.
-HARMLESS_KNOBS = {"MIPGPU_STAGE_STATS", "MIPGPU_WORK_STATS", "MIPGPU_STAGE_TRACE", "MIPGPU_NO_TORCH"}
+HARMLESS_KNOBS = {"MIPGPU_STAGE_STATS", "MIPGPU_WORK_STATS", "MIPGPU_STAGE_TRACE", "MIPGPU_NO_TORCH", "MIPGPU_SLOW_CALLS"}
 
 
 def active_knobs():
