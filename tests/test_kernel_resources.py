@@ -6,9 +6,12 @@ objects' metadata, tests/kernel_resources.py).
 * mip_search_kernel: <= 128 VGPRs, i.e. 4 waves per SIMD -- two 8-wave workgroups per CU
   (or one 16-wave workgroup in small launches), the occupancy the persistent grid is sized
   for.
-* filter_kernel: <= 64 VGPRs (8 waves per SIMD).
+* filter_kernel: 2-D filters (128-thread tiles) <= 64 VGPRs, i.e. 8 waves per SIMD; the
+  separable ones run one-wave 64-thread tiles (round 6) whose ~10 KB of LDS each allow 16 per
+  CU, 4 waves per SIMD: <= 128 VGPRs.
 """
 import os
+import re
 
 import pytest
 
@@ -51,4 +54,5 @@ def test_search_kernel_occupancy(kernels):
 
 def test_filter_kernel_occupancy(kernels):
     for name, k in _named(kernels, "filter_kernel").items():
-        assert k[".vgpr_count"] <= 64, (name, k[".vgpr_count"])
+        sep = re.search(r"filter_kernelILi\dELb\dELb(\d)EE", name).group(1) == "1"  # <RAD, FLOAT, SEP>
+        assert k[".vgpr_count"] <= (128 if sep else 64), (name, k[".vgpr_count"])
