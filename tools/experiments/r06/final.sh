@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 6 final GPU pass: tests + smoke + kernel trace / PMC + bench line + small launches
+# (tools/final_round.sh), the config sweep, the multi-rank rehearsal (end-to-end legs at N > 1),
+# queued one-frame calls merged / not, and the engine sequence with the device block cache.
+set -uo pipefail
+cd "$(dirname "$0")/../../.."
+O=gpurun_out/r06final; mkdir -p $O
+OUT=$O bash tools/final_round.sh || exit 1
+echo "== config sweep $(date +%T)"
+OUT=$O bash tools/config_sweep.sh > $O/configs.log 2>&1 || { tail -20 $O/configs.log; exit 1; }
+tail -3 $O/configs.log | cut -c1-300
+echo "== multirank $(date +%T)"
+OUT=$O bash tools/multirank_rehearsal.sh > $O/multirank.log 2>&1 || { tail -20 $O/multirank.log; exit 1; }
+grep -E "^==|aggregate" $O/multirank.log | cut -c1-300
+echo "== merge rates $(date +%T)"
+OUTTAG=r06final/merge DDS=1 bash tools/experiments/r06/k.sh > $O/merge.log 2>&1 || { tail -20 $O/merge.log; exit 1; }
+tail -12 $O/merge.log
+echo "== done $(date +%T)"
