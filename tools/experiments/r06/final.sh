@@ -1,11 +1,11 @@
 #!/bin/bash
 # Round 6 final GPU pass: tests + smoke + kernel trace / PMC + bench line + small launches
 # (tools/final_round.sh), the config sweep, the multi-rank rehearsal (end-to-end legs at N > 1),
-# queued one-frame calls merged / not, and the engine sequence with the device block cache.
+# queued one-frame calls merged / not.  Two gpurun calls: final.sh a, then final.sh b.
 set -uo pipefail
 cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06final; mkdir -p $O
-OUT=$O bash tools/final_round.sh || exit 1
+if [ "${1:-a}" = a ]; then OUT=$O bash tools/final_round.sh; exit $?; fi
 echo "== config sweep $(date +%T)"
 OUT=$O bash tools/config_sweep.sh > $O/configs.log 2>&1 || { tail -20 $O/configs.log; exit 1; }
 tail -3 $O/configs.log | cut -c1-300
