@@ -40,12 +40,17 @@ constexpr int kClassW[kNumClasses] = {64, 32, 32, 16, 32, 8, 16, 16, 8, 32, 4, 1
                                       4, 4, 4, 8, 8, 8, 32, 16};
 constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4, 16, 8, 4, 8, 4, 8, 16, 8, 16,
                                       32, 16, 8, 32, 16, 16, 16, 32};
-// MIP_SIX_WAVES (round 5): 12-wave search workgroups, two per CU -- six waves per SIMD instead
-// of four (mip_search.hip: the MIP tables read from global memory, a smaller per-wave scratch,
-// 80 VGPRs); 16x16 and 16x8 CUs then take two row parts (their one-row-part tasks need 1168
-// scratch words).
+// MIP_SIX_WAVES: the search kernel's occupancy design.
+//   3 (default since round 6): 12-wave workgroups, two per CU -- six waves per SIMD (80 VGPRs)
+//     -- with the MIP tables and the next item's window in LDS beside a 768-word per-wave
+//     scratch: 16x16 and 16x8 CUs take two row parts (a one-row-part task needs 1168 words),
+//     8xH tasks produce their reduced predictions in quarters and the 64-slot 4x4 / 4x8 tasks
+//     in halves (mip_search.hip Geo, phase_a_half, walk_pairs_chunked); +2.6-2.9 % against 0.
+//   0: 8-wave workgroups, two per CU, four waves per SIMD, 1280-word scratch (rounds 1-5).
+//   1, 2 (round 5 experiments): 12-wave workgroups with the tables in global memory, 1152-word
+//     scratch, no prefetch / three 8-wave workgroups.
 #ifndef MIP_SIX_WAVES
-#define MIP_SIX_WAVES 0
+#define MIP_SIX_WAVES 3
 #endif
 constexpr int kV16 = MIP_SIX_WAVES ? 2 : 1;  // row parts of the 16x16 / 16x8 base classes
 constexpr int kClassV[kNumClasses] = {4, 2, 1, 2, 1, 1, kV16, kV16, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2, 4,
@@ -184,11 +189,10 @@ struct FilterArgs {
   int kernel_idx;
 };
 
-// Waves per search workgroup: two 8-wave workgroups share a CU in batched launches; small
-// launches can run one 16-wave workgroup per CU instead ("wide"), whose waves share one
-// item's tasks (launch_search).
-// (MIP_SIX_WAVES 1: two 12-wave workgroups per CU; 2: three 8-wave workgroups per CU)
-constexpr int kSearchWaves = MIP_SIX_WAVES == 1 ? 12 : 8, kWideWaves = 16;
+// Waves per search workgroup: two 12-wave workgroups share a CU in batched launches (MIP_SIX_WAVES
+// 3; 8-wave ones with MIP_SIX_WAVES 0, three per CU with 2); small launches can run one 16-wave
+// workgroup per CU instead ("wide"), whose waves share one item's tasks (launch_search).
+constexpr int kSearchWaves = MIP_SIX_WAVES == 1 || MIP_SIX_WAVES == 3 ? 12 : 8, kWideWaves = 16;
 // Workgroups of the search kernel resident on the current device at once (persistent grid
 // size); computed once per engine (mip_engine_create), 0 on error.
 int search_resident_groups(bool alt_refs, bool wide);

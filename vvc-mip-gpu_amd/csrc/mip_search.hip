@@ -7,7 +7,8 @@
 // ~1.2 GB of reduced predictions per 1080p frame, main.cpp:443-444).
 //
 // Work decomposition
-//   workgroup = persistent, 8 waves; takes items = (frame, CTU, quadrant, slice) from a
+//   workgroup = persistent, 12 waves (two per CU: six waves per SIMD, MIP_SIX_WAVES 3; 16 in
+//               small launches, one per CU); takes items = (frame, CTU, quadrant, slice) from a
 //               device-wide queue (one counter per XCD chunk, take_item).  No CU of the 47 shapes straddles a 64x64 quadrant, so
 //               an item stages only its quadrant (+1 row above, +4 columns left: the
 //               reference samples) in LDS; the MIP matrices are staged once per workgroup.
@@ -106,8 +107,14 @@ constexpr int kEntryBytes = 16;                         // 8 f16 MFMA inputs per
 constexpr int kCuTableBytes = 64 * kEntryBytes;
 #ifndef MIP_SCRATCH_WORDS
 // 1152 with six waves per SIMD: two 12-wave workgroups per CU in 160 KB of LDS
-#define MIP_SCRATCH_WORDS (MIP_SIX_WAVES == 1 ? 1152 : (MIP_SIX_WAVES == 2 ? 1144 : 1280))
+// (MIP_SIX_WAVES 3, round 6: 768, the MIP tables kept in LDS, the 64-slot 4xN and the 8xH
+// tasks' reduced predictions produced in chunks of two rows, see Geo)
+#define MIP_SCRATCH_WORDS \
+  (MIP_SIX_WAVES == 1 ? 1152 : (MIP_SIX_WAVES == 2 ? 1144 : (MIP_SIX_WAVES == 3 ? 768 : 1280)))
 #endif
+// Chunks that end inside a CU's block pair or 4x4 block (MIP_SIX_WAVES 3): phase A of the next
+// chunk runs in the middle of the lane's walk (walk_pairs_chunked, walk_4x4_chunked).
+constexpr bool kSpanChunks = MIP_SIX_WAVES == 3;
 constexpr int kScratchWords = MIP_SCRATCH_WORDS;        // [slot][position] packed mode pairs
 constexpr int kWaveBytes = kCuTableBytes + kScratchWords * 4;
 constexpr int kWaveStride = kWaveBytes;  // LDS bytes between waves' private areas
@@ -198,9 +205,15 @@ struct Geo {
   static constexpr int V = VP;                        // row parts per CU
   static constexpr int SLOTS = 64 / (S * V);          // CUs per task
   static constexpr int KV = R / V;                    // upsampling windows per row part
-  // 8xH: the reduced predictions of all the task's CUs do not fit the scratch: two halves
-  static constexpr bool CHUNKED = SID == 2 && UH == 1 && 64 / (S * V) * (64 + 4) > kScratchWords;
-  static constexpr int CPOS = CHUNKED ? 32 : NOUT;    // scratch positions per chunk
+  // Classes without horizontal interpolation whose reduced predictions for all the task's CUs
+  // do not fit the scratch produce them in chunks of CROWS reduced rows: 8xH in two halves
+  // (four quarters with MIP_SIX_WAVES 3), the 64-slot 4x4 / 4x8 tasks (MIP_SIX_WAVES 3) in two.
+  static constexpr int CROWS = UH != 1 || 64 / (S * V) * (NOUT + 4) <= kScratchWords ? R
+                               : !kSpanChunks ? (SID == 2 ? R / 2 : R)
+                               : 64 / (S * V) * (NOUT / 2 + 4) > kScratchWords ? R / 4 : R / 2;
+  static constexpr bool CHUNKED = CROWS < R;
+  static constexpr int NCH = R / CROWS;               // chunks
+  static constexpr int CPOS = CROWS * R;              // scratch positions per chunk (UH == 1: rows of R)
   // Scratch rows: classes with horizontal interpolation (UH > 1) keep the anchor row's left
   // boundary sample in front of each reduced row (position k*RP, reduced (k, kx) at
   // k*RP + kx + 1), so the interpolation reads "the sample before" without a select.
@@ -215,6 +228,7 @@ struct Geo {
   static_assert(SLOTS * PITCH <= kScratchWords, "scratch");
   // a row part is whole upsampling windows and whole 4x4 blocks
   static_assert(V == 1 || (!CHUNKED && SID != 0 && (UV >= 4 || KV % (4 / UV) == 0)), "row parts");
+  static_assert(!CHUNKED || (CROWS >= 2 && (kSpanChunks || (SID == 2 && NCH == 2))), "chunks");
 };
 
 // ---- reference samples -------------------------------------------------------------
@@ -851,7 +865,8 @@ __device__ __forceinline__ void walk_strip(const ORIG &orig, const RED &red, int
 #endif
 template <int W, int H, int V>
 constexpr bool kPaired = Geo<W, H, V>::SID != 0 && W * H >= MIP_PAIR_MIN_AREA && V == kClassV[size_class(W, H)] &&
-                         ((Geo<W, H, V>::CHUNKED ? 4 * Geo<W, H, V>::UV : Geo<W, H, V>::KV * Geo<W, H, V>::UV) / 4) % 2 == 0;
+                         ((Geo<W, H, V>::CHUNKED && !kSpanChunks ? Geo<W, H, V>::CROWS * Geo<W, H, V>::UV
+                                                                 : Geo<W, H, V>::KV * Geo<W, H, V>::UV) / 4) % 2 == 0;
 
 template <int W, int H, int V, class ORIG, class RED>
 __device__ __forceinline__ void walk_pairs(const ORIG &orig, const RED &red, int x0, int k0, s2 (&prev)[4],
@@ -943,6 +958,117 @@ __device__ __forceinline__ void walk_pairs(const ORIG &orig, const RED &red, int
   }
 }
 
+// MIP_SIX_WAVES 3 (kSpanChunks): walks whose chunks of reduced rows end inside a block or a
+// block pair.  sw(c) runs phase A of chunk c (wave-synchronised on both sides); the partial
+// block / block A's residuals and the vertical-pass state stay in registers across it.
+// 4x4: rows 0, 1 from chunk 0, rows 2, 3 from chunk 1.
+template <int W, int H, int V, class ORIG, class RED, class SW, class ACC>
+__device__ __forceinline__ void walk_4x4_chunked(const ORIG &orig, RED red, SW &sw, ACC &acc) {
+  static_assert(Geo<W, H, V>::SID == 0 && Geo<W, H, V>::CROWS == 2, "4x4 chunks");
+  typename ORIG::Block b;
+  static_for<4>([&](auto i_c) {
+    constexpr int i = decltype(i_c)::value;
+    if constexpr (i == 2) {
+      sw(1);
+      red.k0 = -2;
+    }
+    s2 prow[4];
+    red.row4(i, 0, prow);
+    block_row<i>(b, prow, orig(i));
+  });
+  u2 sad, satd;
+  block_finish(b, sad, satd);
+  acc.add(sad, satd);
+}
+
+// Paired walk over all of the lane's rows (V = 1) with a chunk switch before every anchor row
+// k that starts a chunk (k % CROWS == 0, k > 0); otherwise as walk_pairs.
+template <int W, int H, int V, class ORIG, class RED, class SW>
+__device__ __forceinline__ void walk_pairs_chunked(const ORIG &orig, RED red, int x0, s2 (&prev)[4], PairAcc &acc,
+                                                   SW &sw) {
+  using G = Geo<W, H, V>;
+  static_assert(G::CHUNKED && G::UV >= 2 && V == 1, "chunked pairs");
+  constexpr int NBP = G::KV * G::UV / 8;  // block pairs
+  auto at = [&](int k) {                  // k: wave-uniform
+    if (k > 0 && k % G::CROWS == 0) {
+      sw(k / G::CROWS);
+      red.k0 = -k;
+    }
+  };
+#pragma unroll 1
+  for (int bp = 0; bp < NBP; bp++) {
+    uint32_t dA[16], t0[16], t1[16];
+    const int yb = 8 * bp;  // CU row of A's first row
+    auto emit = [&](auto i_c, const s2 (&prow)[4]) {
+      constexpr int i = decltype(i_c)::value;
+      if constexpr (i < 4) {
+        uint32_t d[4];
+        residual_row<i>(prow, orig(yb + i), d);
+#pragma unroll
+        for (int c = 0; c < 4; c++) dA[4 * i + c] = d[c];
+      } else {
+        uint32_t dB[4];
+        residual_row<i - 4>(prow, orig(yb + i), dB);
+        if constexpr (ORIG::TR) pair_row_tr<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
+        else pair_row<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
+      }
+    };
+    if constexpr (G::UV == 2) {
+      const int kb = yb / 2;  // windows kb..kb+3
+      static_for<4>([&](auto w_c) {
+        constexpr int w = decltype(w_c)::value;
+        s2 next[4], mid[4];
+        at(kb + w);
+        anchor_row<W, H>(red, kb + w, x0, next);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) mid[cc] = avg_round(prev[cc], next[cc]);
+        emit(std::integral_constant<int, 2 * w>{}, mid);
+        emit(std::integral_constant<int, 2 * w + 1>{}, next);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
+      });
+    } else {
+      constexpr int NWIN = G::UV == 4 ? 2 : 1;
+      static_for<NWIN>([&](auto w_c) {
+        constexpr int w = decltype(w_c)::value;
+        const int k = yb / G::UV + w;
+        s2 next[4];
+        at(k);
+        anchor_row<W, H>(red, k, x0, next);
+        uint32_t delta[4], num[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+          delta[cc] = as_u32(next[cc]) - as_u32(prev[cc]);
+          num[cc] = as_u32(pk_mad_cc<G::UV, G::UV / 2>(as_u2(prev[cc])));
+        }
+        static_for<G::UV>([&](auto r_c) {
+          constexpr int r = decltype(r_c)::value, o = r + 1;
+          s2 prow[4];
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            if constexpr (o == G::UV) {
+              prow[cc] = next[cc];
+            } else {
+              num[cc] += delta[cc];
+              prow[cc] = as_s2(as_u2(num[cc]) >> (u2){G::LV, G::LV});
+            }
+          }
+          emit(std::integral_constant<int, w * G::UV + r>{}, prow);
+        });
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) prev[cc] = next[cc];
+      });
+    }
+    if constexpr (ORIG::TR) {
+      acc.t0 = pair_finish_tr(t0, acc.t0);
+      acc.t1 = pair_finish_tr(t1, acc.t1);
+    } else {
+      acc.t0 = pair_finish(t0, acc.t0);
+      acc.t1 = pair_finish(t1, acc.t1);
+    }
+  }
+}
+
 struct Ctx {
   const SearchArgs *a;
   const uint16_t *org;        // quadrant tile of original samples
@@ -972,8 +1098,14 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   using G = Geo<W, H, V>;
   const int r = lane & 15, h = lane >> 4;
   const int m0 = TR ? 2 * q - G::MODES : 2 * q;
+  // MIP_SIX_WAVES 3 chunks of two reduced rows: sizeId 0/1 (one 16-output block holds the
+  // whole 4x4 prediction) compute it for each chunk and store that chunk's two rows (HALF);
+  // transposed 8xH take the outputs of rows 2*chunk, 2*chunk + 1, all 8 columns (TR2:
+  // matrix row r -> output 8 * (r >> 1) + (r & 1) + 2 * chunk, column r >> 1).
+  constexpr bool HALF = G::CHUNKED && G::SID != 2;
+  constexpr bool TR2 = TR && G::SID == 2 && G::CHUNKED && G::CROWS == 2;
   // A: coefficient row of mode m0 + (h >> 1), inputs 4*(h & 1)..+3
-  const int jrow = (G::SID == 2 && TR) ? 8 * (r >> 2) + (r & 3) : r;
+  const int jrow = TR2 ? 8 * (r >> 1) + (r & 1) : (G::SID == 2 && TR) ? 8 * (r >> 2) + (r & 3) : r;
   const uint8_t *abase = x.w + ((G::WBASE + (m0 + (h >> 1)) * G::NOUT + jrow) * 8 + 4 * (h & 1)) * 2;
   // B: column r = (slot 8*cs + r/2, mode r&1), nonzero only in the K half of its mode
   const bool bsel = (h >> 1) == (r & 1);
@@ -989,18 +1121,22 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
   constexpr int NCS = (G::SLOTS + 7) / 8;  // column sets (8 CUs x 2 modes) of a full task
   // column sets holding CUs (scalar: the task's CU count is wave-uniform)
   const int ncs_run = __builtin_amdgcn_readfirstlane((ncu + 7) >> 3);
-  constexpr int NRB = G::CPOS / 16;        // 16-row blocks in this chunk
+  constexpr int NRB = HALF ? 1 : G::CPOS / 16;  // 16-row blocks in this chunk
   // the lane's 4 results of block rb sit at stored positions pos0 + i * PSTEP
-  // (padded rows: position (k, kx) at k*RP + kx + 1; outputs 4h..4h+3 share one row)
+  // (padded rows: position (k, kx) at k*RP + kx + 1; outputs 4h..4h+3 share one row;
+  // TR2: row i & 1, column 2h + (i >> 1) of the chunk)
   constexpr int PSTEP = TR ? G::RP : 1;
-  const int pos0 = TR ? h + G::PAD : (G::PAD ? (4 * h / G::R) * G::RP + (4 * h) % G::R + 1 : 4 * h);
+  const int pos0 = TR2 ? 2 * h : TR ? h + G::PAD : (G::PAD ? (4 * h / G::R) * G::RP + (4 * h) % G::R + 1 : 4 * h);
   uint8_t *lane_dst = x.wave + kCuTableBytes + ((r >> 1) * G::PITCH + pos0) * 4 + 2 * (r & 1);
 #pragma unroll
   for (int rb = 0; rb < NRB; rb++) {
     int jofs, pofs;  // uniform: matrix row offset, stored-position offset of the block
-    if constexpr (G::SID == 2) {
-      const int rbg = G::CHUNKED ? 2 * chunk + rb : rb;  // 16-row block 0..3 of the matrix
-      const int cofs = G::CHUNKED ? 32 * chunk : 0;
+    if constexpr (TR2) {
+      jofs = 2 * chunk;
+      pofs = 0;
+    } else if constexpr (G::SID == 2) {
+      const int rbg = G::CHUNKED ? NRB * chunk + rb : rb;  // 16-row block 0..3 of the matrix
+      const int cofs = G::CHUNKED ? G::CPOS * chunk : 0;
       if constexpr (!TR) {
         jofs = 16 * rbg;
         pofs = G::PAD ? 2 * rbg * G::RP : 16 * rbg - cofs;
@@ -1011,7 +1147,7 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
       }
     } else {
       jofs = 0;
-      pofs = 0;
+      pofs = HALF ? -8 * chunk : 0;  // rows 2 * chunk, 2 * chunk + 1 -> chunk rows 0, 1
     }
     const h4 av = *reinterpret_cast<const h4 *>(abase + jofs * 16);
     // classes with many column sets (one row block): all B operands read up front, so the
@@ -1029,22 +1165,80 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
       const f4 d = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bv, cin, 0, 0, 0);
       // columns of slots >= ncu hold garbage; they land in unused scratch columns unless
       // the class has fewer than 8 slots
-      if (G::SLOTS % 8 == 0 || 8 * cs + (r >> 1) < ncu) {
+      if ((G::SLOTS % 8 == 0 || 8 * cs + (r >> 1) < ncu) && (!HALF || TR || (h >> 1) == chunk)) {
         uint8_t *dst = lane_dst + (pofs + 8 * cs * G::PITCH) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const uint32_t v = floor_sat(d[i]);  // < 2^16; the upper clip is applied by Red
-          *reinterpret_cast<uint16_t *>(dst + i * PSTEP * 4) = (uint16_t)v;
-        }
+        static_for<4>([&](auto i_c) {
+          constexpr int i = decltype(i_c)::value;
+          constexpr int off = TR2 ? (i & 1) * G::R + (i >> 1) : i * PSTEP;
+          if (!(HALF && TR) || (i >> 1) == chunk) {
+            const uint32_t v = floor_sat(d[i]);  // < 2^16; the upper clip is applied by Red
+            *reinterpret_cast<uint16_t *>(dst + off * 4) = (uint16_t)v;
+          }
+        });
       }
     }
   }
 }
 
+// Phase A of one chunk (two reduced rows) of a 64-slot sizeId 0 / 1 task (MIP_SIX_WAVES 3:
+// 4x4, 4x8).  Both modes of a pair read the same boundary vector (a pair is either untransposed
+// or transposed), so the chunk's 8 outputs of both modes become the 16 matrix rows
+// (row r = (mode r >> 3, chunk output r & 7)) and the columns 16 CUs: 4 MFMAs per chunk, every
+// result stored once (the block-diagonal layout of phase_a would compute all 16 outputs of 8
+// CUs per MFMA and keep half).  K: the 8 inputs in the first half, zeros in the second.
+// Chunk output t of rows {2c, 2c + 1}: untransposed j = 8c + t at chunk position t; transposed
+// (stored at (j % 4, j / 4)) j = 4 (t >> 1) + 2c + (t & 1) at position 4 (t & 1) + (t >> 1).
+template <int W, int H, int V, bool TR>
+__device__ __forceinline__ void phase_a_half(const Ctx &x, int lane, int q, int chunk) {
+  using G = Geo<W, H, V>;
+  static_assert(G::CHUNKED && G::SID != 2 && G::SLOTS == 64 && G::CROWS == 2 && !G::PAD, "half chunks");
+  const int r = lane & 15, h = lane >> 4;
+  const int m0 = TR ? 2 * q - G::MODES : 2 * q;
+  auto jout = [&](int t) { return TR ? 4 * (t >> 1) + 2 * chunk + (t & 1) : 8 * chunk + t; };
+  // A: row r, inputs 4h..4h+3 (h < 2); B: CU 16 cs + r, inputs 4h..4h+3 (h < 2)
+  const uint8_t *aptr = h < 2 ? x.w + ((G::WBASE + (m0 + (r >> 3)) * G::NOUT + jout(r & 7)) * 8 + 4 * h) * 2 : x.zero;
+  const h4 av = *reinterpret_cast<const h4 *>(aptr);
+  const uint8_t *bbase = h < 2 ? x.wave + r * kEntryBytes + 8 * (h ^ (TR ? 1 : 0)) : x.zero;
+  const int bstep = h < 2 ? 16 * kEntryBytes : 0;
+  // C: rows 4h..4h+3 = mode h >> 1, chunk outputs 4 (h & 1) + i
+  const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1) +
+                    (m0 + (h >> 1)) * G::NOUT;
+  const int t0 = 4 * (h & 1);
+  f4 cin;
+  if constexpr (TR) {
+    const float2 lo = *reinterpret_cast<const float2 *>(ct + jout(t0)), hi = *reinterpret_cast<const float2 *>(ct + jout(t0 + 2));
+    cin = f4{lo.x, lo.y, hi.x, hi.y};
+  } else {
+    cin = *reinterpret_cast<const f4 *>(ct + jout(t0));
+  }
+  h4 bvs[4];
+#pragma unroll
+  for (int cs = 0; cs < 4; cs++) bvs[cs] = *reinterpret_cast<const h4 *>(bbase + cs * bstep);
+  // the lane's results: CU 16 cs + r, mode h >> 1, chunk outputs t0 + i
+  uint8_t *lane_dst = x.wave + kCuTableBytes + (r * G::PITCH) * 4 + 2 * (h >> 1);
+#pragma unroll
+  for (int cs = 0; cs < 4; cs++) {
+    const f4 d = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bvs[cs], cin, 0, 0, 0);
+    uint8_t *dst = lane_dst + 16 * cs * G::PITCH * 4;  // slots >= ncu: unused scratch rows
+    static_for<4>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      const int t = t0 + i;
+      const int pos = TR ? 4 * (t & 1) + (t >> 1) : t;
+      *reinterpret_cast<uint16_t *>(dst + pos * 4) = (uint16_t)floor_sat(d[i]);
+    });
+  }
+}
+
 template <int W, int H, int V>
 __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, int chunk) {
-  if (q >= Geo<W, H>::MODES / 2) phase_a<W, H, V, true>(x, lane, ncu, q, chunk);
-  else phase_a<W, H, V, false>(x, lane, ncu, q, chunk);
+  using G = Geo<W, H, V>;
+  if constexpr (G::CHUNKED && G::SID != 2) {
+    if (q >= G::MODES / 2) phase_a_half<W, H, V, true>(x, lane, q, chunk);
+    else phase_a_half<W, H, V, false>(x, lane, q, chunk);
+  } else {
+    if (q >= Geo<W, H>::MODES / 2) phase_a<W, H, V, true>(x, lane, ncu, q, chunk);
+    else phase_a<W, H, V, false>(x, lane, ncu, q, chunk);
+  }
 }
 
 // Sum over aligned groups of N adjacent lanes, delivered to the last lane of each group:
@@ -1171,7 +1365,19 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_ti
     for (int cc = 0; cc < 4; cc++) prev[cc] = top[cc];
     phase_a<W, H, V>(x, lane, ncu, q, 0);
     wave_lds_sync();
-    if constexpr (PAIRED && G::CHUNKED) {
+    if constexpr (kSpanChunks && G::CHUNKED) {
+      auto sw = [&](int c) {
+        wave_lds_sync();  // every lane is done with the previous chunk
+        phase_a<W, H, V>(x, lane, ncu, q, c);
+        wave_lds_sync();
+      };
+      if constexpr (G::SID == 0) {
+        walk_4x4_chunked<W, H, V>(orig, red, sw, acc);
+      } else {
+        static_assert(PAIRED, "chunked classes walk block pairs");
+        walk_pairs_chunked<W, H, V>(orig, red, x0, prev, acc, sw);
+      }
+    } else if constexpr (PAIRED && G::CHUNKED) {
       walk_pairs<W, H, V>(orig, red, x0, 0, prev, acc);
       wave_lds_sync();
       phase_a<W, H, V>(x, lane, ncu, q, 1);
@@ -1346,8 +1552,11 @@ struct WindowStager {
 // frame are not the reference's (the packed 16-bit / f16 arithmetic is sized for 10 bits), so
 // the host reports the search as failed.  Rare path: one plain store per offending thread.
 // Merged chunks (SearchArgs::frame_status): the frame's own call's status set.
+#ifndef MIP_FRAME_STATUS
+#define MIP_FRAME_STATUS 1  // A/B: 0 = one status set per launch (wrong statuses in merged launches)
+#endif
 __device__ __forceinline__ void flag_above_10_bits(uint32_t bits, const SearchArgs &a, int frame, int word) {
-  if (bits & kAbove10Bits) (a.frame_status ? a.frame_status[frame] : a.status)[word] = 1u;
+  if (bits & kAbove10Bits) (MIP_FRAME_STATUS && a.frame_status ? a.frame_status[frame] : a.status)[word] = 1u;
 }
 
 template <int NT>
@@ -1674,8 +1883,14 @@ __device__ __forceinline__ void pair_loop(const SearchArgs &a, uint16_t *org_buf
 #ifndef MIP_TABLES_GLOBAL
 #define MIP_TABLES_GLOBAL 0  // A/B: the MIP tables from global memory at four waves per SIMD too
 #endif
-constexpr bool kTablesInLds = !MIP_SIX_WAVES && !MIP_TABLES_GLOBAL;
-constexpr bool kPrefetchKernel = !MIP_SIX_WAVES;
+constexpr bool kTablesInLds = (!MIP_SIX_WAVES || MIP_SIX_WAVES == 3) && !MIP_TABLES_GLOBAL;
+// (MIP_SIX_WAVES 3: two windows, the tables and 12 x 4 KB of wave areas fill 81 648 of the
+// 81 920 bytes a workgroup may take with two per CU)
+#ifndef MIP_S6_PF
+#define MIP_S6_PF 1  // A/B: next-item prefetch in the MIP_SIX_WAVES 3 build
+#endif
+#define MIP_PF_KERNEL (!MIP_SIX_WAVES || (MIP_SIX_WAVES == 3 && MIP_S6_PF))
+constexpr bool kPrefetchKernel = MIP_PF_KERNEL;
 template <bool ALT, bool DEC, bool PF_, int NW>
 __global__ __launch_bounds__(64 * NW, NW == kWideWaves ? 4 : MIP_WAVES_PER_EU) void mip_search_kernel(SearchArgs a) {
   constexpr bool PF = PF_ && !ALT && NW == kSearchWaves && kPrefetchKernel;
@@ -1913,11 +2128,18 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
 
 }  // namespace
 
+constexpr size_t search_lds_bytes_c(bool alt, bool pf, int waves) {
+  return (size_t)(((pf || waves == kWideWaves) && !alt ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 +
+         (kTablesInLds ? kTableBytes : 0) + kZeroBytes + (size_t)waves * kWaveStride + kCounterWords * 4;
+}
 size_t search_lds_bytes(bool alt, bool pf, int waves) {
   const bool two = (pf || waves == kWideWaves) && !alt;  // kOrgTiles
   return (size_t)((two ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 + (kTablesInLds ? kTableBytes : 0) + kZeroBytes +
          (size_t)waves * kWaveStride + kCounterWords * 4;
 }
+
+static_assert(!MIP_SIX_WAVES || MIP_SIX_WAVES == 2 ||
+                  search_lds_bytes_c(false, MIP_PF_KERNEL, kSearchWaves) * 2 <= 160 * 1024, "two workgroups per CU");
 
 template <bool ALT, bool DEC, bool PF, int NW>
 static int resident_per_cu() {
@@ -1939,7 +2161,7 @@ int search_resident_groups(bool alt, bool wide) {
   else
     per_cu = alt ? std::min(resident_per_cu<true, false, false, S>(), resident_per_cu<true, true, false, S>())
                  : std::min({resident_per_cu<false, false, false, S>(), resident_per_cu<false, true, false, S>(),
-#if MIP_PREFETCH_MIN_ITEMS < 1000000 && !MIP_SIX_WAVES  // (builds that never prefetch: the others' grid)
+#if MIP_PREFETCH_MIN_ITEMS < 1000000 && MIP_PF_KERNEL  // (builds that never prefetch: the others' grid)
                              resident_per_cu<false, false, true, S>(), resident_per_cu<false, true, true, S>()
 #endif
                              });

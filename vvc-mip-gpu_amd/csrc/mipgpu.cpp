@@ -726,7 +726,7 @@ double lpt_makespan(const std::vector<double> &order_cost, int nframes, int grou
 }
 
 // Small launches on 16-wave workgroups, one per CU (MIPGPU_WIDE: 0 = never, 1 = every small
-// launch; default: below kWideItemsPerGroup items per CU at one slice).  Two 8-wave workgroups
+// launch; default: below kWideItemsPerGroup items per CU at one slice).  Two 8-wave workgroups (round 4)
 // on a CU progress at very different rates when both run an item (the SIMD arbiter serves the
 // older waves first: 98 vs 170 us for the two items of a CU in a 1080p frame,
 // profiles/r04_item_timeline_1frame.csv), so a launch of ~2 items per CU ends with one
