@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Opcode histogram of the innermost (mode-pair) loop of one size class's search kernel
-(compile-only, -DMIP_ONLY_CLASS): tools/loop_isa.py CLASS [ALT] [--dump FILE]."""
+(compile-only, -DMIP_ONLY_CLASS): tools/loop_isa.py CLASS [ALT] [--dump FILE]; extra -D options
+in the KNOBS environment variable (e.g. KNOBS=-DMIP_SIX_WAVES=0)."""
 import collections
 import os
 import re
@@ -13,10 +14,13 @@ alt = len(sys.argv) > 2 and sys.argv[2] == "1"
 out = "/tmp/loop_class_%d.s" % cls
 subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + REPO + "/include",
                        "-I" + REPO + "/vvc-mip-gpu_amd/csrc", "-DMIP_ONLY_CLASS=%d" % cls, "--cuda-device-only", "-S",
-                       "-o", out, REPO + "/vvc-mip-gpu_amd/csrc/mip_search.hip"], stderr=subprocess.DEVNULL)
+                       "-o", out, REPO + "/vvc-mip-gpu_amd/csrc/mip_search.hip"] + os.environ.get("KNOBS", "").split(),
+                      stderr=subprocess.DEVNULL)
 s = open(out).read()
-name = "_ZN6mipgpu12_GLOBAL__N_117mip_search_kernelILb%dELb0ELb%dEEEvNS_10SearchArgsE:" % ((1, 0) if alt else (0, 1))
-start = s.index(name)
+# the batched kernel (<ALT, table, PF = !ALT, NW = the batched workgroup's waves, not 16)
+m = re.search(r"^(_ZN6mipgpu12_GLOBAL__N_117mip_search_kernelILb%dELb0ELb%dELi(?!16)\d+EEEvNS_10SearchArgsE):" %
+              ((1, 0) if alt else (0, 1)), s, re.M)
+start = m.start()
 body = s[start:s.index("s_endpgm", start)].splitlines()
 # the mode-pair loop: the smallest backward-branch range holding both the phase-A MFMAs
 # and the per-pair cost store

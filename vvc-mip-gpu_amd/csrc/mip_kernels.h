@@ -43,16 +43,15 @@ constexpr int kClassH[kNumClasses] = {64, 32, 16, 32, 8, 32, 16, 8, 16, 4, 32, 4
 // MIP_SIX_WAVES: the search kernel's occupancy design.
 //   3 (default since round 6): 12-wave workgroups, two per CU -- six waves per SIMD (80 VGPRs)
 //     -- with the MIP tables and the next item's window in LDS beside a 768-word per-wave
-//     scratch: 16x16 and 16x8 CUs take two row parts (a one-row-part task needs 1168 words),
-//     8xH tasks produce their reduced predictions in quarters and the 64-slot 4x4 / 4x8 tasks
-//     in halves (mip_search.hip Geo, phase_a_half, walk_pairs_chunked); +2.6-2.9 % against 0.
+//     scratch: 16x16 / 16x8 and the 64-slot 4x4 / 4x8 tasks produce their reduced predictions
+//     in halves, 8xH tasks in quarters (mip_search.hip Geo, phase_a_half, walk_pairs_chunked).
 //   0: 8-wave workgroups, two per CU, four waves per SIMD, 1280-word scratch (rounds 1-5).
 //   1, 2 (round 5 experiments): 12-wave workgroups with the tables in global memory, 1152-word
 //     scratch, no prefetch / three 8-wave workgroups.
 #ifndef MIP_SIX_WAVES
 #define MIP_SIX_WAVES 3
 #endif
-constexpr int kV16 = MIP_SIX_WAVES ? 2 : 1;  // row parts of the 16x16 / 16x8 base classes
+constexpr int kV16 = MIP_SIX_WAVES == 1 || MIP_SIX_WAVES == 2 ? 2 : 1;  // row parts of the 16x16 / 16x8 base classes
 constexpr int kClassV[kNumClasses] = {4, 2, 1, 2, 1, 1, kV16, kV16, 1, 1, 2, 1, 2, 1, 1, 1, 1, 2, 4, 2, 4,
                                       2, 2, 1, 1, 1, 4, 2, 4};
 constexpr bool kClassTR[kNumClasses] = {false, false, false, false, false, false, false, false, false, false, false,

@@ -208,7 +208,9 @@ struct Geo {
   // Classes without horizontal interpolation whose reduced predictions for all the task's CUs
   // do not fit the scratch produce them in chunks of CROWS reduced rows: 8xH in two halves
   // (four quarters with MIP_SIX_WAVES 3), the 64-slot 4x4 / 4x8 tasks (MIP_SIX_WAVES 3) in two.
-  static constexpr int CROWS = UH != 1 || 64 / (S * V) * (NOUT + 4) <= kScratchWords ? R
+  // With horizontal interpolation (padded rows, MIP_SIX_WAVES 3: 16x16, 16x8) in halves.
+  static constexpr int CROWS = UH != 1 ? (kSpanChunks && 64 / (S * V) * (R * (R + 1) + 1) > kScratchWords ? R / 2 : R)
+                               : 64 / (S * V) * (NOUT + 4) <= kScratchWords ? R
                                : !kSpanChunks ? (SID == 2 ? R / 2 : R)
                                : 64 / (S * V) * (NOUT / 2 + 4) > kScratchWords ? R / 4 : R / 2;
   static constexpr bool CHUNKED = CROWS < R;
@@ -221,7 +223,7 @@ struct Geo {
   static constexpr int RP = PAD ? R + 1 : R;
   // scratch: [slot][PITCH] dwords; UH == 1 classes read 4 consecutive positions (16-B aligned)
   // (the 64-slot 4xN classes drop the 4-word pad when it does not fit: 64 x 20 > kScratchWords)
-  static constexpr int PITCH = UH == 1 ? (SLOTS * (CPOS + 4) <= kScratchWords ? CPOS + 4 : CPOS) : R * RP + 1;
+  static constexpr int PITCH = UH == 1 ? (SLOTS * (CPOS + 4) <= kScratchWords ? CPOS + 4 : CPOS) : CROWS * RP + 1;
   static constexpr int WBASE = SID == 2 ? 0 : (SID == 1 ? kWeightRowOffS1 : kWeightRowOffS0);
   static constexpr int MODES = SID == 2 ? 6 : (SID == 1 ? 8 : 16);
   static_assert(SLOTS * S * V == 64, "lanes");
@@ -987,7 +989,7 @@ template <int W, int H, int V, class ORIG, class RED, class SW>
 __device__ __forceinline__ void walk_pairs_chunked(const ORIG &orig, RED red, int x0, s2 (&prev)[4], PairAcc &acc,
                                                    SW &sw) {
   using G = Geo<W, H, V>;
-  static_assert(G::CHUNKED && G::UV >= 2 && V == 1, "chunked pairs");
+  static_assert(G::CHUNKED && V == 1, "chunked pairs");
   constexpr int NBP = G::KV * G::UV / 8;  // block pairs
   auto at = [&](int k) {                  // k: wave-uniform
     if (k > 0 && k % G::CROWS == 0) {
@@ -1013,7 +1015,14 @@ __device__ __forceinline__ void walk_pairs_chunked(const ORIG &orig, RED red, in
         else pair_row<i - 4>(dA + 4 * (i - 4), dB, t0, t1, acc);
       }
     };
-    if constexpr (G::UV == 2) {
+    if constexpr (G::UV == 1) {
+      static_for<8>([&](auto i_c) {
+        s2 prow[4];
+        at(yb + decltype(i_c)::value);
+        anchor_row<W, H>(red, yb + decltype(i_c)::value, x0, prow);
+        emit(i_c, prow);
+      });
+    } else if constexpr (G::UV == 2) {
       const int kb = yb / 2;  // windows kb..kb+3
       static_for<4>([&](auto w_c) {
         constexpr int w = decltype(w_c)::value;
@@ -1137,13 +1146,14 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
     } else if constexpr (G::SID == 2) {
       const int rbg = G::CHUNKED ? NRB * chunk + rb : rb;  // 16-row block 0..3 of the matrix
       const int cofs = G::CHUNKED ? G::CPOS * chunk : 0;
+      const int crow = G::CHUNKED ? G::CROWS * chunk * G::RP : 0;  // padded rows: the chunk's first row
       if constexpr (!TR) {
         jofs = 16 * rbg;
-        pofs = G::PAD ? 2 * rbg * G::RP : 16 * rbg - cofs;
+        pofs = G::PAD ? 2 * rbg * G::RP - crow : 16 * rbg - cofs;
       } else {  // output j = 8*(h + 4*rr) + i + 4*cc -> position (i + 4cc, h + 4rr)
         const int cc = rbg >> 1, rr = rbg & 1;
         jofs = 32 * rr + 4 * cc;
-        pofs = G::PAD ? 4 * cc * G::RP + 4 * rr : 32 * cc + 4 * rr - cofs;
+        pofs = G::PAD ? 4 * cc * G::RP + 4 * rr - crow : 32 * cc + 4 * rr - cofs;
       }
     } else {
       jofs = 0;
@@ -1198,8 +1208,10 @@ __device__ __forceinline__ void phase_a_half(const Ctx &x, int lane, int q, int 
   // A: row r, inputs 4h..4h+3 (h < 2); B: CU 16 cs + r, inputs 4h..4h+3 (h < 2)
   const uint8_t *aptr = h < 2 ? x.w + ((G::WBASE + (m0 + (r >> 3)) * G::NOUT + jout(r & 7)) * 8 + 4 * h) * 2 : x.zero;
   const h4 av = *reinterpret_cast<const h4 *>(aptr);
-  const uint8_t *bbase = h < 2 ? x.wave + r * kEntryBytes + 8 * (h ^ (TR ? 1 : 0)) : x.zero;
-  const int bstep = h < 2 ? 16 * kEntryBytes : 0;
+  // (lanes h >= 2 read the same entries' other half: finite f16 values -- an entry holds
+  // 1024 + b for every input -- times the zero A operand, so those K rows add exactly 0 to
+  // the written CUs' columns; columns of slots >= ncu land in unused scratch rows)
+  const uint8_t *bbase = x.wave + r * kEntryBytes + 8 * ((h & 1) ^ (TR ? 1 : 0));
   // C: rows 4h..4h+3 = mode h >> 1, chunk outputs 4 (h & 1) + i
   const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1) +
                     (m0 + (h >> 1)) * G::NOUT;
@@ -1213,7 +1225,7 @@ __device__ __forceinline__ void phase_a_half(const Ctx &x, int lane, int q, int 
   }
   h4 bvs[4];
 #pragma unroll
-  for (int cs = 0; cs < 4; cs++) bvs[cs] = *reinterpret_cast<const h4 *>(bbase + cs * bstep);
+  for (int cs = 0; cs < 4; cs++) bvs[cs] = *reinterpret_cast<const h4 *>(bbase + cs * 16 * kEntryBytes);
   // the lane's results: CU 16 cs + r, mode h >> 1, chunk outputs t0 + i
   uint8_t *lane_dst = x.wave + kCuTableBytes + (r * G::PITCH) * 4 + 2 * (h >> 1);
 #pragma unroll
@@ -1344,10 +1356,29 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_ti
 #pragma unroll
     for (int cc = 0; cc < 4; cc++) top[cc] = splat(c.top ? t4[cc] : c.padT);
   }
-  if constexpr (G::PAD) {
+  // padded rows in chunks: the lane's left samples stay in registers and each chunk's are
+  // written to its chunk-relative rows (write_left)
+  constexpr int NLV = (G::R + G::S * G::V - 1) / (G::S * G::V);
+  uint32_t lvs[G::PAD && G::CHUNKED ? NLV : 1];
+  uint32_t *lcol = reinterpret_cast<uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
+  auto write_left = [&](int chunk) {
+#pragma unroll
+    for (int j = 0; j < NLV; j++) {
+      const int k = sub + j * G::S * G::V;
+      if (active && k < G::R && k / G::CROWS == chunk) lcol[(k - chunk * G::CROWS) * G::RP] = lvs[j];
+    }
+  };
+  if constexpr (G::PAD && G::CHUNKED) {
+#pragma unroll
+    for (int j = 0; j < NLV; j++) {
+      const int k = sub + j * G::S * G::V;
+      const uint32_t lv = k < G::R && c.left ? rt.left(c.lx - 1, c.ly + k * G::UV + G::UV - 1) : c.padL;
+      lvs[j] = lv | lv << 16;
+    }
+    write_left(0);
+  } else if constexpr (G::PAD) {
     // left boundary sample of anchor row k (CU row k*UV + UV - 1), both halves; phase A
     // never writes these positions
-    uint32_t *lcol = reinterpret_cast<uint32_t *>(x.wave + kCuTableBytes) + cs * G::PITCH;
     for (int k = sub; k < G::R; k += G::S * G::V) {
       const uint32_t lv = c.left ? rt.left(c.lx - 1, c.ly + k * G::UV + G::UV - 1) : c.padL;
       if (active) lcol[k * G::RP] = lv | lv << 16;
@@ -1364,11 +1395,15 @@ __device__ __forceinline__ void run_task(const Ctx &x, const RefTile<LAT> &rt_ti
 #pragma unroll
     for (int cc = 0; cc < 4; cc++) prev[cc] = top[cc];
     phase_a<W, H, V>(x, lane, ncu, q, 0);
+    if constexpr (G::PAD && G::CHUNKED) {
+      if (q > task.q0) write_left(0);  // the previous pair's last chunk left its rows' samples
+    }
     wave_lds_sync();
     if constexpr (kSpanChunks && G::CHUNKED) {
       auto sw = [&](int c) {
         wave_lds_sync();  // every lane is done with the previous chunk
         phase_a<W, H, V>(x, lane, ncu, q, c);
+        if constexpr (G::PAD) write_left(c);
         wave_lds_sync();
       };
       if constexpr (G::SID == 0) {
