@@ -1192,51 +1192,53 @@ __device__ __forceinline__ void phase_a(const Ctx &x, int lane, int ncu, int q, 
 
 // Phase A of one chunk (two reduced rows) of a 64-slot sizeId 0 / 1 task (MIP_SIX_WAVES 3:
 // 4x4, 4x8).  Both modes of a pair read the same boundary vector (a pair is either untransposed
-// or transposed), so the chunk's 8 outputs of both modes become the 16 matrix rows
-// (row r = (mode r >> 3, chunk output r & 7)) and the columns 16 CUs: 4 MFMAs per chunk, every
-// result stored once (the block-diagonal layout of phase_a would compute all 16 outputs of 8
-// CUs per MFMA and keep half).  K: the 8 inputs in the first half, zeros in the second.
-// Chunk output t of rows {2c, 2c + 1}: untransposed j = 8c + t at chunk position t; transposed
-// (stored at (j % 4, j / 4)) j = 4 (t >> 1) + 2c + (t & 1) at position 4 (t & 1) + (t >> 1).
+// or transposed), so the chunk's 8 outputs of both modes become the 16 matrix rows and the
+// columns 16 CUs: 4 MFMAs per chunk, every result stored once (the block-diagonal layout of
+// phase_a would compute all 16 outputs of 8 CUs per MFMA and keep half).  K: the 8 inputs in
+// the first half, zeros in the second.
+// Row r = (mode r & 1, chunk position p = ((r >> 1) >> 1) + 4 ((r >> 1) & 1)), so a lane's
+// four results are both modes of positions h and h + 4 (h = lane >> 4) of CU lane & 15: the
+// 16-bit stores of one instruction hit 64 distinct words of a 12-word pitch (the first
+// version, rows = (mode, position), put two lanes on each word: 54 % LDS bank conflicts in the
+// 4x4 class).  Chunk position p is row p >> 2 (2c + (p >> 2) of the prediction), column p & 3;
+// untransposed it is output j = 8c + p, transposed (stored at (j % 4, j / 4)) output
+// j = 4 (p & 3) + 2c + (p >> 2).
 template <int W, int H, int V, bool TR>
 __device__ __forceinline__ void phase_a_half(const Ctx &x, int lane, int q, int chunk) {
   using G = Geo<W, H, V>;
-  static_assert(G::CHUNKED && G::SID != 2 && G::SLOTS == 64 && G::CROWS == 2 && !G::PAD, "half chunks");
+  static_assert(G::CHUNKED && G::SID != 2 && G::SLOTS == 64 && G::CROWS == 2 && !G::PAD && G::PITCH >= 8, "half chunks");
   const int r = lane & 15, h = lane >> 4;
   const int m0 = TR ? 2 * q - G::MODES : 2 * q;
-  auto jout = [&](int t) { return TR ? 4 * (t >> 1) + 2 * chunk + (t & 1) : 8 * chunk + t; };
+  auto jout = [&](int p) { return TR ? 4 * (p & 3) + 2 * chunk + (p >> 2) : 8 * chunk + p; };
+  auto pos_of_row = [](int row) { return ((row >> 1) >> 1) + 4 * ((row >> 1) & 1); };
   // A: row r, inputs 4h..4h+3 (h < 2); B: CU 16 cs + r, inputs 4h..4h+3 (h < 2)
-  const uint8_t *aptr = h < 2 ? x.w + ((G::WBASE + (m0 + (r >> 3)) * G::NOUT + jout(r & 7)) * 8 + 4 * h) * 2 : x.zero;
+  const uint8_t *aptr = h < 2 ? x.w + ((G::WBASE + (m0 + (r & 1)) * G::NOUT + jout(pos_of_row(r))) * 8 + 4 * h) * 2
+                              : x.zero;
   const h4 av = *reinterpret_cast<const h4 *>(aptr);
   // (lanes h >= 2 read the same entries' other half: finite f16 values -- an entry holds
   // 1024 + b for every input -- times the zero A operand, so those K rows add exactly 0 to
   // the written CUs' columns; columns of slots >= ncu land in unused scratch rows)
   const uint8_t *bbase = x.wave + r * kEntryBytes + 8 * ((h & 1) ^ (TR ? 1 : 0));
-  // C: rows 4h..4h+3 = mode h >> 1, chunk outputs 4 (h & 1) + i
-  const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1) +
-                    (m0 + (h >> 1)) * G::NOUT;
-  const int t0 = 4 * (h & 1);
+  // C: rows 4h + i = (mode i & 1, position h + 4 (i >> 1))
+  const float *ct = reinterpret_cast<const float *>(x.w + kWeightRows * 16) + (G::WBASE - kWeightRowOffS1);
   f4 cin;
-  if constexpr (TR) {
-    const float2 lo = *reinterpret_cast<const float2 *>(ct + jout(t0)), hi = *reinterpret_cast<const float2 *>(ct + jout(t0 + 2));
-    cin = f4{lo.x, lo.y, hi.x, hi.y};
-  } else {
-    cin = *reinterpret_cast<const f4 *>(ct + jout(t0));
-  }
+  static_for<4>([&](auto i_c) {
+    constexpr int i = decltype(i_c)::value;
+    cin[i] = ct[(m0 + (i & 1)) * G::NOUT + jout(h + 4 * (i >> 1))];
+  });
   h4 bvs[4];
 #pragma unroll
   for (int cs = 0; cs < 4; cs++) bvs[cs] = *reinterpret_cast<const h4 *>(bbase + cs * 16 * kEntryBytes);
-  // the lane's results: CU 16 cs + r, mode h >> 1, chunk outputs t0 + i
-  uint8_t *lane_dst = x.wave + kCuTableBytes + (r * G::PITCH) * 4 + 2 * (h >> 1);
+  uint8_t *lane_dst = x.wave + kCuTableBytes + (r * G::PITCH + h) * 4;
 #pragma unroll
   for (int cs = 0; cs < 4; cs++) {
     const f4 d = __builtin_amdgcn_mfma_f32_16x16x16f16(av, bvs[cs], cin, 0, 0, 0);
     uint8_t *dst = lane_dst + 16 * cs * G::PITCH * 4;  // slots >= ncu: unused scratch rows
     static_for<4>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
-      const int t = t0 + i;
-      const int pos = TR ? 4 * (t & 1) + (t >> 1) : t;
-      *reinterpret_cast<uint16_t *>(dst + pos * 4) = (uint16_t)floor_sat(d[i]);
+      // (volatile LDS store: two 16-bit stores, not a v_perm-packed 32-bit one -- VALU is the bound)
+      typedef __attribute__((address_space(3))) volatile uint16_t lds_u16;
+      *(lds_u16 *)(dst + 16 * (i >> 1) + 2 * (i & 1)) = (uint16_t)floor_sat(d[i]);
     });
   }
 }
