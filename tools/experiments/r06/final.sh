@@ -15,4 +15,7 @@ grep -E "^==|aggregate" $O/multirank.log | cut -c1-300
 echo "== merge rates $(date +%T)"
 OUTTAG=r06final/merge DDS=1 bash tools/experiments/r06/k.sh > $O/merge.log 2>&1 || { tail -20 $O/merge.log; exit 1; }
 tail -12 $O/merge.log
+echo "== four-wave vs default $(date +%T)"
+OUTTAG=r06final/ab_s0 S6LIB=vvc-mip-gpu_amd/lib/libmipgpu.so EXTRA_LIBS=tools/bin/lib_s0.so bash tools/experiments/r06/s6.sh > $O/ab_s0.log 2>&1 || { tail -20 $O/ab_s0.log; exit 1; }
+tail -9 $O/ab_s0.log
 echo "== done $(date +%T)"
