@@ -27,11 +27,11 @@ import csv, glob, json, sys
 raw, out = sys.argv[1], sys.argv[2]
 line = json.loads(open(out + "/trace_bench.json").read().strip().splitlines()[-1])
 rows = [r for f in glob.glob(raw + "/**/*kernel_trace.csv", recursive=True) for r in csv.DictReader(open(f))
-        if "mip_search_kernel<false, false, true, 8>" in r["Kernel_Name"]]
+        if "mip_search_kernel<false, false, true, " in r["Kernel_Name"]]  # (12 waves; 8 before round 6)
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 timed = rows[-line["steps"]:]
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
-rec = {"kernel": "mip_search_kernel<false, false, true, 8>", "build_id": line["build_id"], "launches": len(rows),
+rec = {"kernel": rows[0]["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", ""), "build_id": line["build_id"], "launches": len(rows),
        "timed_launches": len(dur), "timed_avg_ms": round(sum(dur) / len(dur), 4), "timed_min_ms": round(min(dur), 4),
        "timed_max_ms": round(max(dur), 4), "bench_ms_per_step_same_run": line["ms_per_step"],
        "bench_kernel_ms_same_run": line["roofline"]["kernel_ms_per_launch"]}

@@ -14,17 +14,21 @@ import sys
 root, key, out = sys.argv[1], sys.argv[2], sys.argv[3]
 COUNTERS = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
             "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_ACTIVE_INST_VALU2")
-SEARCH = "mip_search_kernel<false, false, true, 8>"      # original-reference search (the bench `value`)
+# original-reference search with the prefetch (the bench `value`): 12 waves since round 6 (8 before)
+SEARCH = "mip_search_kernel<false, false, true, "
 FILTER = "filter_kernel<2, true, false>"    # BASELINE configs[2] filter (bench `filter`)
 
 
 def collect(kernel):
     vals = {c: [] for c in COUNTERS}
+    vals["_name"] = set()
     for path in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
         per = {}
         for r in csv.DictReader(open(path)):
             if kernel not in r["Kernel_Name"] or r["Counter_Name"] not in vals:
                 continue
+            vals["_name"].add(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+                              .replace("void ", "").replace("mipgpu::", ""))
             k = (r["Dispatch_Id"], r["Counter_Name"])
             per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
         for (_, c), v in per.items():
@@ -55,7 +59,7 @@ valu, grbm = mean(s_vals, "SQ_INSTS_VALU"), mean(s_vals, "GRBM_GUI_ACTIVE")
 util = valu * 4 / (1024 * grbm / 8) if valu and grbm else None
 dual = mean(s_vals, "SQ_ACTIVE_INST_VALU2")
 conf, lds = mean(s_vals, "SQ_LDS_BANK_CONFLICT"), mean(s_vals, "SQ_LDS_IDX_ACTIVE")
-rec.update({"kernel": SEARCH, "valu_insts_per_launch": valu, "gui_active_cycles_per_xcd": grbm and grbm / 8,
+rec.update({"kernel": ", ".join(sorted(s_vals["_name"])) or SEARCH, "valu_insts_per_launch": valu, "gui_active_cycles_per_xcd": grbm and grbm / 8,
             "valu_issue_utilization": util and round(util, 4),
             "valu_insts_per_simd_quad_cycle": util and round(util, 4),
             "valu_dual_issue_share": dual and valu and round(dual / valu, 4),
