@@ -22,14 +22,24 @@ frames = synth_frames_torch(W, H, max(NF), 0x5B, 0, device=dev)
 s = torch.cuda.Stream(dev)
 
 
+# SB_DEC=1: decisions only (no cost table); SB_FILTER=NAME[:IDX]: the engine's alternative
+# references (filter + search per launch)
+DEC = os.environ.get("SB_DEC") == "1"
+FILT = os.environ.get("SB_FILTER")
+
+
 def run(eng, n, reps=40):
-    c = torch.empty((n, eng.costs_per_frame), dtype=torch.int32, device=dev)
+    if DEC:
+        kw = dict(costs=False, best_mode=torch.empty((n, eng.cus_per_frame), dtype=torch.uint8, device=dev),
+                  best_cost=torch.empty((n, eng.cus_per_frame), dtype=torch.int32, device=dev))
+    else:
+        kw = dict(costs=torch.empty((n, eng.costs_per_frame), dtype=torch.int32, device=dev))
     for _ in range(5):
-        eng.search_device(frames[:n], costs=c, stream=s)
+        eng.search_device(frames[:n], stream=s, **kw)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
-        eng.search_device(frames[:n], costs=c, stream=s)
+        eng.search_device(frames[:n], stream=s, **kw)
     e1.record(s)
     torch.cuda.synchronize(dev)
     return e0.elapsed_time(e1) / reps
@@ -48,10 +58,13 @@ for cut, wide, order, sl in grid:
         os.environ.pop("MIPGPU_WIDE", None)
     else:
         os.environ["MIPGPU_WIDE"] = wide
-    eng = MipEngine(W, H, max_batch=max(NF), slices_per_ctu=sl)
+    fkw = {}
+    if FILT:
+        fkw = dict(filter=FILT.split(":")[0], kernel_idx=int(FILT.split(":")[1]) if ":" in FILT else 0)
+    eng = MipEngine(W, H, max_batch=max(NF), slices_per_ctu=sl, **fkw)
     res = {n: round(run(eng, n), 4) for n in NF}
     eng.close()
-    print(json.dumps({"cut": float(cut), "wide": wide, "order": "lpt" if order == "1" else "raster",
+    print(json.dumps({"cut": float(cut), "wide": wide, "dec": DEC, "filter": FILT, "order": "lpt" if order == "1" else "raster",
                       "slices": sl or "auto",
                       "ms_per_launch": res,
                       "frames_per_s": {n: round(n / (ms * 1e-3), 1) for n, ms in res.items()}}), flush=True)

@@ -693,6 +693,12 @@ bool dec_inline() {
   return e && *e == '1';
 }
 
+// MIPGPU_PIPE_GRID=0 (A/B knob): alternating host-pipeline chunks keep the full grid.
+bool pipe_half_grid() {
+  const char *e = getenv("MIPGPU_PIPE_GRID");
+  return !(e && *e == '0');
+}
+
 // MIPGPU_EXT_DONE=0 (A/B knob): record the host pipeline's per-chunk completion event as a
 // separate marker instead of on the search kernel's dispatch.
 bool ext_done_enabled() {
@@ -734,7 +740,10 @@ double lpt_makespan(const std::vector<double> &order_cost, int nframes, int grou
 // Measured (profiles/r04_small_batch_wide.jsonl): 1 frame 0.185 -> 0.175 ms, 2 frames
 // 0.293 -> 0.314 ms (without a second workgroup the item tails and window stagings idle the
 // CU), 8-16 frames -9 %.
-constexpr int kWideItemsPerGroup = 4;
+// Round 6 (six-wave 12-wave workgroups, tools/experiments/r06/small_ab.sh): 2-frame launches
+// (3.98 items per CU) 0.2905 ms on 12-wave workgroups vs 0.2967 wide, 1 frame 0.1758 vs 0.1743
+// -- the threshold moved from 4 to 3 items per CU (only one-frame 1080p launches go wide).
+constexpr int kWideItemsPerGroup = 3;
 bool wide_launch(long long items1, int cus) {
   if (cus < 1) return false;  // no 16-wave workgroup fits a CU of this device
   const char *e = getenv("MIPGPU_WIDE");
@@ -1319,7 +1328,7 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
                               int32_t *d_best_cost, hipStream_t s, bool caller_refs, uint32_t *d_status,
                               int ctu0 = 0, int nrange = -1, uint32_t *split_acc = nullptr,
                               mipgpu::SplitArgs *defer_split = nullptr, hipEvent_t *done = nullptr,
-                              uint32_t *const *frame_status = nullptr) {
+                              uint32_t *const *frame_status = nullptr, bool alternating = false) {
   if (!e || !d_frames || nframes < 1) return fail("bad search arguments");
   // Decisions only (no cost table): the search writes each CU's decision into d_best /
   // d_best_cost; CUs whose mode pairs are cut over several tasks keep a packed running argmin
@@ -1357,7 +1366,16 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   a.sad = d_sad;
   a.satd = d_satd;
   const mip_engine::Work &work = pick_work(e, nframes, nrange, alt);
-  const int resident = work.wide ? e->resident_wide[alt ? 1 : 0] : e->resident[alt ? 1 : 0];
+  int resident = work.wide ? e->resident_wide[alt ? 1 : 0] : e->resident[alt ? 1 : 0];
+  // Host-pipeline chunks whose searches alternate between the two search streams and are too
+  // small to prefetch (round 6): one workgroup per CU instead of two.  Consecutive chunks then
+  // share every CU -- at six waves per SIMD a full grid left no room for the next chunk's
+  // workgroups nor for the download stream's unpacking / copy kernels, which waited for the
+  // search to drain (8 queued one-frame decisions-only calls 4650 -> 5050 frames/s, 32 calls
+  // 4650-5570 -> 6500, tools/experiments/r06/merge_knobs.sh MIPGPU_GROUPS=256).
+  if (alternating && !work.wide && pipe_half_grid() &&
+      (long long)4 * work.slices * nrange * nframes < (long long)kSmallLaunchItemsPerGroup * resident)
+    resident = std::max(1, resident / 2);
   a.tasks = work.d_tasks;
   a.jobs = work.d_jobs;
   a.list_begin = work.d_lists;
@@ -1574,7 +1592,7 @@ static int flush_open(mip_engine *e) {
     if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
                            (sig & kSigRefs) != 0, call_status(e, first), 0, -1,
                            defer ? e->d_split_acc + fo * e->nctus * MIP_CUS_PER_CTU : nullptr, defer ? &split : nullptr,
-                           &comp_done, e->d_frame_status + row) != 0)
+                           &comp_done, e->d_frame_status + row, search_streams() == 2) != 0)
       return -1;
     if (comp_done) HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     e->last_slot = sl;
@@ -1934,7 +1952,7 @@ static int search_frames_chunks(mip_engine *e, const uint16_t *frames, const uin
     if (search_device_impl(e, d_frames, d_refs, nb, d_costs, d_sad, d_satd, d_best, d_best_cost, comp,
                            refs_or_null != nullptr, call_status(e, call), 0, -1,
                            defer ? e->d_split_acc + fo * e->nctus * MIP_CUS_PER_CTU : nullptr,
-                           defer ? &split : nullptr, &comp_done) != 0)
+                           defer ? &split : nullptr, &comp_done, nullptr, alt_streams) != 0)
       return -1;
     if (comp_done) HIP_TRY(hipEventRecord(e->slot_comp[sl], comp));
     e->last_slot = sl;
