@@ -7,7 +7,8 @@ objects' metadata, tests/kernel_resources.py).
   (item setup and window staging, once per quadrant item: none inside the size classes' code,
   tools/isa_dump.py); they are held to 96 bytes per lane.
 * mip_search_kernel: the 12-wave variants <= 80 VGPRs, i.e. 6 waves per SIMD -- two 12-wave
-  workgroups per CU; the 16-wave variants (small launches, one workgroup per CU) <= 128 VGPRs,
+  workgroups per CU; the 16-wave variants (small launches, one workgroup per CU) and the
+  four-wave twin's 8-wave ones (the host pipeline's small chunks, two per CU) <= 128 VGPRs,
   4 waves per SIMD: the occupancy the persistent grid is sized for.
 * filter_kernel: 2-D filters (128-thread tiles) <= 64 VGPRs, i.e. 8 waves per SIMD; the
   separable ones run one-wave 64-thread tiles (round 6) whose ~10 KB of LDS each allow 16 per
@@ -39,7 +40,8 @@ def _named(kernels, part):
 def test_every_kernel_variant_present(kernels):
     # {orig, alt} x {table, decisions} x prefetch (orig), and the 16-wave variants of small
     # launches ({orig, alt} x {table, decisions}, no prefetch)
-    assert len(_named(kernels, "mip_search_kernel")) == 10
+    # + the four-wave twin's 8-wave variants ({orig, alt} x {table, decisions}, orig x prefetch)
+    assert len(_named(kernels, "mip_search_kernel")) == 16
     assert len(_named(kernels, "filter_kernel")) == 8      # radius x int/float x 2-D/separable
     for part in ("fixup_kernel", "best_mode_kernel", "dec_split_kernel"):
         _named(kernels, part)
@@ -60,9 +62,9 @@ def test_search_kernel_occupancy(kernels):
     for name, k in _named(kernels, "mip_search_kernel").items():
         nw = _search_waves(name)
         waves.add(nw)
-        limit = 80 if nw == 12 else 128  # 6 / 4 waves per SIMD
+        limit = 80 if nw == 12 else 128  # 6 / 4 waves per SIMD (8: the four-wave twin)
         assert k[".vgpr_count"] + k.get(".agpr_count", 0) <= limit, (name, k[".vgpr_count"])
-    assert waves == {12, 16}
+    assert waves == {8, 12, 16}
 
 
 def test_filter_kernel_occupancy(kernels):

@@ -19,6 +19,8 @@ pids=()
 for s in mip_search mip_filter mip_fixup; do
   /opt/rocm/bin/hipcc $F -c -o "$tmp/$s.o" "csrc/$s.hip" & pids+=($!)
 done
+/opt/rocm/bin/hipcc $F -DMIP_SIX_WAVES=0 -DMIP_FOUR_WAVE_TWIN=1 -c -o "$tmp/mip_search_four.o" csrc/mip_search.hip \
+  2> >(grep -v "macro redefined\|^ *[0-9]* | \|^ *| \|note: previous definition\|warning generated\|^<command line>" >&2) & pids+=($!)
 /opt/rocm/bin/hipcc $F "-DMIPGPU_BUILD_ID=\"$id\"" -c -o "$tmp/mipgpu.o" csrc/mipgpu.cpp & pids+=($!)
 for p in "${pids[@]}"; do wait "$p" || { echo "build_variant: a compile failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$out" "$tmp"/*.o

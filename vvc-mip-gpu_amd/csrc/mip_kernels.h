@@ -195,10 +195,20 @@ constexpr int kSearchWaves = MIP_SIX_WAVES == 1 || MIP_SIX_WAVES == 3 ? 12 : 8, 
 // Workgroups of the search kernel resident on the current device at once (persistent grid
 // size); computed once per engine (mip_engine_create), 0 on error.
 int search_resident_groups(bool alt_refs, bool wide);
+// The four-wave twin (mip_search.hip compiled again with -DMIP_SIX_WAVES=0
+// -DMIP_FOUR_WAVE_TWIN=1): 8-wave workgroups, two per CU, for the host pipeline's small
+// alternating chunks; same arguments, no wide launches (0 / hipErrorInvalidValue).
+#if !defined(MIP_FOUR_WAVE_TWIN) || !MIP_FOUR_WAVE_TWIN  // (in the twin the names above are these)
+int search_resident_groups_four(bool alt_refs, bool wide);
+#endif
 // done: optional event recorded by the kernel's own dispatch (hipExtLaunchKernel's stop
 // event) instead of a separate marker packet behind it.
 hipError_t launch_search(const SearchArgs &a, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s,
                          hipEvent_t done = nullptr);
+#if !defined(MIP_FOUR_WAVE_TWIN) || !MIP_FOUR_WAVE_TWIN
+hipError_t launch_search_four(const SearchArgs &a, int nframes, bool alt_refs, int resident, bool wide, hipStream_t s,
+                         hipEvent_t done = nullptr);
+#endif
 hipError_t launch_best_modes(const BestArgs &a, hipStream_t s);
 // Decisions only, CUs whose mode pairs are cut over several tasks (split CUs of the CTU's
 // variant: [split_begin[v], split_begin[v+1]) of `split`, at most max_split per variant):

@@ -37,6 +37,20 @@
 
 #include <hip/hip_ext.h>
 
+// The four-wave twin (round 6): this file compiled a second time with -DMIP_SIX_WAVES=0
+// -DMIP_FOUR_WAVE_TWIN=1 (Makefile: build/mip_search_four.o) exports the 8-wave search as
+// launch_search_four / search_resident_groups_four, which the host pipeline uses for its small
+// alternating chunks (mipgpu.cpp search_device_impl).  The helper kernels live in the
+// primary compilation only.
+#ifndef MIP_FOUR_WAVE_TWIN
+#define MIP_FOUR_WAVE_TWIN 0
+#endif
+#if MIP_FOUR_WAVE_TWIN
+#define launch_search launch_search_four
+#define search_resident_groups search_resident_groups_four
+#define search_lds_bytes search_lds_bytes_four
+#endif
+
 #include "mip_kernels.h"
 #include "mip_tables.h"
 
@@ -49,7 +63,7 @@ typedef _Float16 __attribute__((ext_vector_type(2))) h2;
 typedef _Float16 __attribute__((ext_vector_type(4))) h4;
 typedef float __attribute__((ext_vector_type(4))) f4;
 
-__constant__ mip_shape_desc c_shapes[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;
+[[maybe_unused]] __constant__ mip_shape_desc c_shapes[MIP_NUM_SHAPES] = MIP_SHAPE_TABLE;  // (helper kernels)
 // first CU (reference order inside a CTU) of every shape, for the decision-list kernel
 struct ShapeStarts {
   uint16_t v[MIP_NUM_SHAPES + 1];
@@ -61,7 +75,7 @@ constexpr ShapeStarts make_shape_starts() {
   return st;
 }
 static_assert(make_shape_starts().v[MIP_NUM_SHAPES] == MIP_CUS_PER_CTU, "shape table");
-__constant__ ShapeStarts c_shape_start = make_shape_starts();
+[[maybe_unused]] __constant__ ShapeStarts c_shape_start = make_shape_starts();
 
 #ifndef MIP_PREFETCH_MIN_ITEMS
 #define MIP_PREFETCH_MIN_ITEMS 32  // items per workgroup from which a launch prefetches (A/B knob)
@@ -2116,6 +2130,7 @@ __device__ __forceinline__ void topk_row(const int32_t *row, int k, uint8_t *mo,
 }
 
 // Per-CU decision lists (k = 1: the argmin).
+#if !MIP_FOUR_WAVE_TWIN
 __global__ __launch_bounds__(256) void best_mode_kernel(BestArgs a) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= a.total_cus) return;
@@ -2163,9 +2178,10 @@ __global__ __launch_bounds__(256) void dec_split_kernel(SplitArgs a, int total) 
   }
 }
 
+#endif  // !MIP_FOUR_WAVE_TWIN
 }  // namespace
 
-constexpr size_t search_lds_bytes_c(bool alt, bool pf, int waves) {
+static constexpr size_t search_lds_bytes_c(bool alt, bool pf, int waves) {  // (internal: differs per compilation)
   return (size_t)(((pf || waves == kWideWaves) && !alt ? 2 : 1) * kTileElems + (alt ? kLatElems : 0)) * 2 +
          (kTablesInLds ? kTableBytes : 0) + kZeroBytes + (size_t)waves * kWaveStride + kCounterWords * 4;
 }
@@ -2192,7 +2208,8 @@ int search_resident_groups(bool alt, bool wide) {
   // every variant of a width shares the grid size
   constexpr int S = kSearchWaves, L = kWideWaves;
   int per_cu;
-  if (wide)
+  if (wide && MIP_FOUR_WAVE_TWIN) return 0;
+  if (wide && !MIP_FOUR_WAVE_TWIN)
     per_cu = alt ? std::min(resident_per_cu<true, false, false, L>(), resident_per_cu<true, true, false, L>())
                  : std::min(resident_per_cu<false, false, false, L>(), resident_per_cu<false, true, false, L>());
   else
@@ -2231,11 +2248,15 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   const size_t lds = search_lds_bytes(alt_refs, pf, wide ? kWideWaves : kSearchWaves);
   const dim3 grid(groups);
   constexpr int S = kSearchWaves, L = kWideWaves;
+  (void)L;
   auto go = [&](auto kern, const dim3 &block) {  // with `done`: the dispatch itself records it (no marker packet)
     if (done) hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)lds, s, nullptr, done, 0u, a);
     else hipLaunchKernelGGL(kern, grid, block, lds, s, a);
   };
   if (wide) {
+#if MIP_FOUR_WAVE_TWIN
+    return hipErrorInvalidValue;  // (the twin serves batched-width launches only)
+#else
     const dim3 block(64 * L);
     if (alt_refs) {
       if (dec) go(mip_search_kernel<true, true, false, L>, block);
@@ -2245,6 +2266,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
       else go(mip_search_kernel<false, false, false, L>, block);
     }
     return hipGetLastError();
+#endif
   }
   const dim3 block(64 * S);
   if (alt_refs) {
@@ -2260,6 +2282,7 @@ hipError_t launch_search(const SearchArgs &args, int nframes, bool alt_refs, int
   return hipGetLastError();
 }
 
+#if !MIP_FOUR_WAVE_TWIN
 hipError_t launch_dec_split(const SplitArgs &a, int nframes, bool init, hipStream_t s) {
   if (a.max_split < 1) return hipSuccess;  // no split CUs
   const long long total = (long long)nframes * a.nrange * a.max_split;
@@ -2275,5 +2298,6 @@ hipError_t launch_best_modes(const BestArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(best_mode_kernel, dim3((a.total_cus + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }
+#endif  // !MIP_FOUR_WAVE_TWIN
 
 }  // namespace mipgpu

@@ -584,6 +584,7 @@ struct mip_engine {
   int nfixup[kMaps] = {};
   int resident[2] = {0, 0};  // persistent search grid (workgroups resident on this device), [alt]
   int resident_wide[2] = {0, 0};  // the same for 16-wave workgroups
+  int resident_four[2] = {0, 0};  // the four-wave twin's (8-wave workgroups; 0: not available)
   // Engine-owned reference scratch d_refs, written by the engine filter when a device-API
   // search has no caller references: every such search records refs_done on its stream, and
   // the next writer of d_refs (another device-API search, on any stream, or a host-API call)
@@ -693,10 +694,12 @@ bool dec_inline() {
   return e && *e == '1';
 }
 
-// MIPGPU_PIPE_GRID=0 (A/B knob): alternating host-pipeline chunks keep the full grid.
-bool pipe_half_grid() {
-  const char *e = getenv("MIPGPU_PIPE_GRID");
-  return !(e && *e == '0');
+// MIPGPU_PIPE_KERNEL (A/B knob) for the host pipeline's small alternating chunks: 4 (default)
+// = the four-wave twin, 6 = the six-wave kernel on one workgroup per CU, 0 = the six-wave
+// kernel's full grid.
+int pipe_kernel() {
+  const char *e = getenv("MIPGPU_PIPE_KERNEL");
+  return e && (*e == '0' || *e == '6') ? *e - '0' : 4;
 }
 
 // MIPGPU_EXT_DONE=0 (A/B knob): record the host pipeline's per-chunk completion event as a
@@ -1197,6 +1200,7 @@ int mip_engine_create(int device, int width, int height, const mip_opts *opts, m
       return cleanup(fail("cannot size the persistent search grid on device %d", device));
     // 16-wave workgroups (small launches) are optional: 0 when one does not fit a CU
     e->resident_wide[alt] = mipgpu::search_resident_groups(alt != 0, true);
+    e->resident_four[alt] = mipgpu::search_resident_groups_four(alt != 0, false);
   }
   ALLOC(e->d_best_cost, ncu * o.best_k * 4);
   ALLOC(e->d_split_acc, ncu * 4);
@@ -1368,14 +1372,19 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const mip_engine::Work &work = pick_work(e, nframes, nrange, alt);
   int resident = work.wide ? e->resident_wide[alt ? 1 : 0] : e->resident[alt ? 1 : 0];
   // Host-pipeline chunks whose searches alternate between the two search streams and are too
-  // small to prefetch (round 6): one workgroup per CU instead of two.  Consecutive chunks then
-  // share every CU -- at six waves per SIMD a full grid left no room for the next chunk's
-  // workgroups nor for the download stream's unpacking / copy kernels, which waited for the
-  // search to drain (8 queued one-frame decisions-only calls 4650 -> 5050 frames/s, 32 calls
-  // 4650-5570 -> 6500, tools/experiments/r06/merge_knobs.sh MIPGPU_GROUPS=256).
-  if (alternating && !work.wide && pipe_half_grid() &&
-      (long long)4 * work.slices * nrange * nframes < (long long)kSmallLaunchItemsPerGroup * resident)
-    resident = std::max(1, resident / 2);
+  // small to prefetch (round 6).  At six waves per SIMD a full grid of the batched kernel
+  // leaves no room on a CU for the next chunk's workgroups nor for the download stream's
+  // unpacking / copy kernels, which wait for the search to drain (a kernel trace of 8 merged
+  // one-frame calls: dec_split busy 1.3 ms instead of 28 us).  Such chunks run the four-wave
+  // twin (8-wave workgroups, two per CU: the occupancy rounds 1-5 ran the whole pipeline at),
+  // or -- MIPGPU_PIPE_KERNEL=6 -- one 12-wave workgroup per CU (8 queued one-frame
+  // decisions-only calls 4740 -> 5100 frames/s, 32 calls 5550 -> 6340).
+  const bool pipe_small = alternating && !work.wide &&
+                          (long long)4 * work.slices * nrange * nframes < (long long)kSmallLaunchItemsPerGroup * resident;
+  const int pk = pipe_kernel();
+  const bool four = pipe_small && pk == 4 && e->resident_four[alt ? 1 : 0] > 0;
+  if (four) resident = e->resident_four[alt ? 1 : 0];
+  else if (pipe_small && pk == 6) resident = std::max(1, resident / 2);
   a.tasks = work.d_tasks;
   a.jobs = work.d_jobs;
   a.list_begin = work.d_lists;
@@ -1448,7 +1457,8 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const bool last = !(alt && e->nfixup[map]) && !engine_refs && !timing &&
                     (decisions_only ? defer_split != nullptr : !(d_best || d_best_cost)) && ext_done_enabled();
   hipEvent_t stop = done && last ? *done : nullptr;
-  const hipError_t le = SLOW_CALL(mipgpu::launch_search(a, nframes, alt, resident, work.wide, s, stop));
+  const hipError_t le = four ? SLOW_CALL(mipgpu::launch_search_four(a, nframes, alt, resident, false, s, stop))
+                             : SLOW_CALL(mipgpu::launch_search(a, nframes, alt, resident, work.wide, s, stop));
   if (le == hipSuccess && stop) *done = nullptr;
   if (le != hipSuccess) {
     ring.failed(slot);  // the pair is cleared before its next use
