@@ -694,12 +694,13 @@ bool dec_inline() {
   return e && *e == '1';
 }
 
-// MIPGPU_PIPE_KERNEL (A/B knob) for the host pipeline's small alternating chunks: 4 (default)
-// = the four-wave twin, 6 = the six-wave kernel on one workgroup per CU, 0 = the six-wave
-// kernel's full grid.
+// MIPGPU_PIPE_KERNEL (A/B knob) for the host pipeline's chunks: 4 (default) = the four-wave
+// twin for small alternating chunks and for decisions-only chunks, 8 = the twin for every
+// chunk, 6 = the six-wave kernel on one workgroup per CU for small alternating chunks, 0 = the
+// six-wave kernel's full grid throughout.
 int pipe_kernel() {
   const char *e = getenv("MIPGPU_PIPE_KERNEL");
-  return e && (*e == '0' || *e == '6') ? *e - '0' : 4;
+  return e && (*e == '0' || *e == '6' || *e == '8') ? *e - '0' : 4;
 }
 
 // MIPGPU_EXT_DONE=0 (A/B knob): record the host pipeline's per-chunk completion event as a
@@ -1382,7 +1383,12 @@ static int search_device_impl(mip_engine *e, const uint16_t *d_frames, const uin
   const bool pipe_small = alternating && !work.wide &&
                           (long long)4 * work.slices * nrange * nframes < (long long)kSmallLaunchItemsPerGroup * resident;
   const int pk = pipe_kernel();
-  const bool four = pipe_small && pk == 4 && e->resident_four[alt ? 1 : 0] > 0;
+  // (decisions-only pipeline chunks of any size too: their downloads -- blit kernels on torch's
+  // runtime -- and split unpacking run beside the next chunk's search; 8 queued 128-frame
+  // calls 7097-7121 -> 7191-7247 frames/s, tools/experiments/r06/e2e_twin.sh; full-table
+  // chunks are PCIe-bound either way and keep the six-wave kernel)
+  const bool four = ((pk == 4 && (pipe_small || (decisions_only && done))) || (pk == 8 && done)) && !work.wide &&
+                    e->resident_four[alt ? 1 : 0] > 0;
   if (four) resident = e->resident_four[alt ? 1 : 0];
   else if (pipe_small && pk == 6) resident = std::max(1, resident / 2);
   a.tasks = work.d_tasks;
