@@ -874,18 +874,22 @@ def test_merged_launches_keep_each_call_its_own(gpu_available, monkeypatch, filt
                 assert np.array_equal(res["cost"][i], oc), (f0, kind, i)
 
 
-def test_merged_launches_1080p_default_policy(gpu_available):
+def test_merged_launches_1080p_default_policy(gpu_available, monkeypatch):
     """Default merge policy at the bench size: 24 one-frame 1080p calls queued back to back
     (page-locked, decisions only and full tables in runs) merge while the pipeline is busy;
     every output equals a synchronous search of the same frame.  Then a one-frame call queued
     behind a 4-frame call stays open after that search has completed, until mip_flush -- or
-    the next call, which finds the GPU idle -- launches it."""
+    the next call, which finds the GPU idle -- launches it.  The reference search runs the
+    six-wave kernel throughout (MIPGPU_PIPE_KERNEL=0), the queued calls the four-wave twin
+    (default for small alternating and decisions-only chunks): the two kernels agree."""
     import time
     from mipgpu import pinned_empty
     W, H = 1920, 1080
     pool = synth_frames(W, H, 4, 0x6E7, 0)
+    monkeypatch.setenv("MIPGPU_PIPE_KERNEL", "0")
     with MipEngine(W, H, max_batch=4) as ref_eng:
         want = ref_eng.search(pool, best=True)
+    monkeypatch.delenv("MIPGPU_PIPE_KERNEL")
     with MipEngine(W, H, max_batch=8) as eng:
         pf = pinned_empty(pool.shape, np.uint16)
         pf[:] = pool
