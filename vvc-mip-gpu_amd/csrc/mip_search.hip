@@ -1299,6 +1299,9 @@ __device__ __forceinline__ uint32_t pin_sum(uint32_t v) {
 // Cost-table stores of a task: a buffer descriptor over the CTU's block (uniform per
 // item), the CU's byte offset as the per-lane VGPR offset (per task) and the mode pair's
 // offset as the scalar offset (per pair) -- the pair loop computes no per-lane address.
+#ifndef MIP_COST_STORE_AUX
+#define MIP_COST_STORE_AUX 0  // A/B: cache-policy bits of the cost-row stores
+#endif
 struct CtuRows {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ explicit CtuRows(int32_t *ctu_block) {
@@ -1306,7 +1309,7 @@ struct CtuRows {
   }
   __device__ __forceinline__ void store(uint32_t cu_ofs, int mq, int v0, int v1) const {
     typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)v0, (unsigned)v1}, r, (int)cu_ofs, mq * 4, 0);
+    __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)v0, (unsigned)v1}, r, (int)cu_ofs, mq * 4, MIP_COST_STORE_AUX);
   }
 };
 
