@@ -31,7 +31,7 @@ def main():
         m = re.match(r"^([0-9a-f]+ )?<(.+)>:$", line)
         if m:
             keep = want in m.group(2)
-        if keep:
+        if keep and "file format" not in line:
             lines.append(re.sub(r"<.*\+0x[0-9a-f]+>", "<L>", line.split("//")[0].rstrip()))
     open(out, "w").write("\n".join(lines) + "\n")
     print(out, len(lines), "lines")
