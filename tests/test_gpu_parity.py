@@ -802,9 +802,9 @@ def test_idle_call_chunks_fit_their_slot(gpu_available, max_batch, n):
             assert np.array_equal(dec["best_mode"][f], bm) and np.array_equal(dec["best_cost"][f], bc), (offset, f)
 
 
-@pytest.mark.parametrize("filt,k,pk", [(None, 0, "4"), ("filterFrame_2d_float_5x5_quarterCtu", 2, "4"), (None, 0, "6"),
-                                       (None, 0, "0")])
-def test_merged_launches_keep_each_call_its_own(gpu_available, monkeypatch, filt, k, pk):
+@pytest.mark.parametrize("filt,k,pk,gather", [(None, 0, "4", "1"), ("filterFrame_2d_float_5x5_quarterCtu", 2, "4", "1"),
+                                              (None, 0, "6", "1"), (None, 0, "0", "0")])
+def test_merged_launches_keep_each_call_its_own(gpu_available, monkeypatch, filt, k, pk, gather):
     """Merged launches (mipgpu.cpp open chunk, ABI 7): small page-locked calls share one search
     launch.  MIPGPU_MERGE=hold makes the grouping deterministic (chunks open even into an idle
     pipeline and are launched only by the other triggers): four decisions-only calls, three
@@ -813,10 +813,12 @@ def test_merged_launches_keep_each_call_its_own(gpu_available, monkeypatch, filt
     equals the oracle, the bad call -- and only it -- fails at its own wait, and the counters
     show exactly four merged launches of 13 calls.  pk: the kernel of these small alternating
     chunks (MIPGPU_PIPE_KERNEL: 4 the four-wave twin, 6 the six-wave kernel on half the grid,
-    0 its full grid) -- the per-frame status pointers work in each."""
+    0 its full grid) -- the per-frame status pointers work in each; gather: the merged
+    decisions-only downloads as one copy kernel (default) or one copy per member buffer."""
     from mipgpu import pinned_empty
     monkeypatch.setenv("MIPGPU_MERGE", "hold")
     monkeypatch.setenv("MIPGPU_PIPE_KERNEL", pk)
+    monkeypatch.setenv("MIPGPU_GATHER_DOWN", gather)  # merged decisions-only downloads: one copy kernel / per member
     w, h = 264, 136
     n = 23
     frames = synth_frames(w, h, n, 0x3E6 + (k or 0), 0)

@@ -470,6 +470,27 @@ __global__ __launch_bounds__(256) void copy_kernel(const uint4 *__restrict__ src
 
 }  // namespace
 
+// One workgroup row per piece (blockIdx.y); 16-byte words where both ends are 16-byte aligned,
+// then the tail bytes.
+__global__ __launch_bounds__(256) void gather_copy_kernel(CopyPieces a) {
+  if ((int)blockIdx.y >= a.n) return;
+  const CopyPiece c = a.p[blockIdx.y];
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x, t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t n16 = (((uintptr_t)c.src | (uintptr_t)c.dst) & 15) == 0 ? c.bytes / 16 : 0;
+  for (uint64_t i = t0; i < n16; i += step) reinterpret_cast<uint4 *>(c.dst)[i] = reinterpret_cast<const uint4 *>(c.src)[i];
+  for (uint64_t i = n16 * 16 + t0; i < c.bytes; i += step) c.dst[i] = c.src[i];
+}
+
+hipError_t launch_gather_copy(const CopyPieces &a, hipStream_t s) {
+  if (a.n < 1) return hipSuccess;
+  if (a.n > kMaxCopyPieces) return hipErrorInvalidValue;
+  uint64_t most = 0;
+  for (int i = 0; i < a.n; i++) most = std::max<uint64_t>(most, a.p[i].bytes);
+  const unsigned bx = (unsigned)std::min<uint64_t>(64, std::max<uint64_t>(1, (most / 16 + 255) / 256));
+  hipLaunchKernelGGL(gather_copy_kernel, dim3(bx, (unsigned)a.n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_copy(const void *src, void *dst, size_t bytes, hipStream_t s) {
   if (bytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16) return hipErrorInvalidValue;
   int dev = 0, cus = 0;

@@ -229,6 +229,19 @@ hipError_t launch_dec_split(const SplitArgs &a, int nframes, bool init, hipStrea
 hipError_t launch_filter(const FilterArgs &a, hipStream_t s);
 // Streaming device-to-device copy (16-byte aligned, multiple of 16 bytes): HBM calibration.
 hipError_t launch_copy(const void *src, void *dst, size_t bytes, hipStream_t s);
+// Several copies in one launch (the merged chunks' downloads into the members' page-locked,
+// device-mapped host buffers: one dispatch instead of one per buffer).
+struct CopyPiece {
+  const uint8_t *src;
+  uint8_t *dst;
+  uint64_t bytes;
+};
+constexpr int kMaxCopyPieces = 64;
+struct CopyPieces {
+  CopyPiece p[kMaxCopyPieces];
+  int n;
+};
+hipError_t launch_gather_copy(const CopyPieces &a, hipStream_t s);
 // Exact per-CU search of `n` CUs of every frame (same outputs as the search kernel: cost /
 // SAD / SATD tables or, decisions only, the decision in a.best_mode / a.best_cost).
 hipError_t launch_fixup(const SearchArgs &a, const FixupCu *cus, int n, int nframes, hipStream_t s);

@@ -694,6 +694,12 @@ bool dec_inline() {
   return e && *e == '1';
 }
 
+// MIPGPU_GATHER_DOWN=0 (A/B knob): merged decisions-only chunks download member by member.
+bool gather_down() {
+  const char *e = getenv("MIPGPU_GATHER_DOWN");
+  return !(e && *e == '0');
+}
+
 // MIPGPU_PIPE_KERNEL (A/B knob) for the host pipeline's chunks: 4 (default) = the four-wave
 // twin for small alternating chunks and for decisions-only chunks, 8 = the twin for every
 // chunk, 6 = the six-wave kernel on one workgroup per CU for small alternating chunks, 0 = the
@@ -1618,7 +1624,34 @@ static int flush_open(mip_engine *e) {
     e->stat_merged_calls += o.members.size();
     HIP_TRY(hipStreamWaitEvent(down, e->slot_comp[sl], 0));
     if (defer) HIP_TRY(mipgpu::launch_dec_split(split, nb, false, down));
+    // Decisions-only members' downloads as one copy kernel writing straight into their
+    // device-mapped page-locked buffers: one dispatch per chunk instead of two copies per
+    // member.  Fewer queued commands, fewer of the runtime's host stalls (section 6 of
+    // DESIGN.md): 32 queued one-frame calls' rounds 6397-6419 frames/s at the 25th percentile
+    // instead of 4033-6187 (medians 6451-6477 vs 6423-6628; tools/experiments/r06/gather.sh).
+    bool gathered = false;
+    if (dec && gather_down() && 2 * o.members.size() <= (size_t)mipgpu::kMaxCopyPieces) {
+      mipgpu::CopyPieces cp{};
+      gathered = true;
+      for (const mip_engine::Member &m : o.members) {
+        const size_t f = (size_t)m.f0, n = (size_t)m.n;
+        auto add = [&](void *host, const void *dev, size_t bytes) {
+          void *dp = nullptr;
+          if (!host) return;
+          if (hipHostGetDevicePointer(&dp, host, 0) != hipSuccess || !dp) {
+            (void)hipGetLastError();
+            gathered = false;
+            return;
+          }
+          cp.p[cp.n++] = mipgpu::CopyPiece{static_cast<const uint8_t *>(dev), static_cast<uint8_t *>(dp), bytes};
+        };
+        add(m.best_mode, d_best + f * upf, n * upf);
+        add(m.best_cost, d_best_cost + f * upf, n * upf * 4);
+      }
+      if (gathered) HIP_TRY(mipgpu::launch_gather_copy(cp, down));
+    }
     for (const mip_engine::Member &m : o.members) {
+      if (gathered) break;
       const size_t f = (size_t)m.f0, n = (size_t)m.n;
       if (m.costs) HIP_TRY(hipMemcpyAsync(m.costs, d_costs + f * cpf, n * cpf * 4, hipMemcpyDeviceToHost, down));
       if (m.sad) HIP_TRY(hipMemcpyAsync(m.sad, d_sad + f * cpf, n * cpf * 4, hipMemcpyDeviceToHost, down));
