@@ -2,7 +2,7 @@
 # Round 6: small ALT launches on the four-wave twin vs the six-wave kernel (MIPGPU_PIPE_KERNEL=0):
 # device-API launches of 1-16 frames and the configs[2] / [4] steps.  Ran with a since-reverted
 # mipgpu.cpp rule (alt_small: ALT launches under kSmallLaunchItemsPerGroup items per workgroup
-# took the twin); result and why it was dropped: DESIGN.md section 9.
+# took the twin); result and why it was dropped: DESIGN.md section 6 (configs sweep).
 set -uo pipefail
 cd "$(dirname "$0")/../../.."
 for envs in "X=1" "MIPGPU_PIPE_KERNEL=0" "X=2" "MIPGPU_PIPE_KERNEL=0"; do
